@@ -1,0 +1,211 @@
+#!/usr/bin/env python3
+"""Benchmark: chain-leapfrog-steps/s of the RHMC hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): 48x48 image, 1 star,
+4096 chains per GPU, fp64.  One bench "step" = one launch of the fused
+leapfrog kernel advancing every chain by `--leap` (default 500) implicit
+generalized-leapfrog steps (sampler_RHMC.py:522-566); chain states stay
+resident in HBM and carry over from launch to launch.
+
+value = total chain-leapfrog-steps over all ranks / max-over-ranks wall time.
+
+Extra objects on the JSON line:
+  roofline      algorithmic HBM bytes per chain-step (SURVEY §8(d):
+                2*N_pix*8 + 4*3K*8 = 36,960 B at C2) x chain-steps per launch
+                / average launch time, HIP events on the launch stream;
+                peak 8.0 TB/s.  `traffic` = measured HBM bytes per launch from
+                profiles/*.json (rocprofv3 PMC), or null.
+  cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on the host cores, one
+                chain per process, bounded sample (rank 0, N=1 only).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2]
+       (N>1: launched by torch.distributed.run, one rank per GPU)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "hmc-stellar-toy-model_amd"))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP64_PEAK_TFLOPS = 78.6    # MI355X FP64 vector (spec)
+
+
+def alg_bytes_per_step(npix, K):
+    return 2 * npix * 8 + 4 * 3 * K * 8
+
+
+def alg_flops_per_step(npix, K):
+    return 2 * npix * (18 * K + 2)
+
+
+def _cpu_worker(args):
+    D, par, q0, p0, nsteps = args
+    import numpy as np  # noqa: F401
+    from oracle.rhmc_ref import RefModel
+    m = RefModel(D, par)
+    t = time.perf_counter()
+    m.trajectory(q0, p0, nsteps, par["delta"], par["counter_max"], record=False)
+    return time.perf_counter() - t
+
+
+def cpu_baseline(wl, seconds_target=15.0):
+    """Time the NumPy port, one chain per process (multiprocessing.Pool)."""
+    import multiprocessing as mp
+    os.environ["OMP_NUM_THREADS"] = "1"
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count()
+    cores = max(1, min(cores, 16))
+    par = dict(wl.params)
+    par["rows"] = par["cols"] = wl.D.shape[0]
+    # calibrate one chain on this core
+    t = _cpu_worker((wl.D, par, wl.q0[0], wl.p0[0], 20))
+    per_step = t / 20
+    nsteps = max(20, int(seconds_target / per_step / 2))
+    jobs = [(wl.D, par, wl.q0[c % wl.n_chains], wl.p0[c % wl.n_chains], nsteps)
+            for c in range(2 * cores)]
+    ctx = mp.get_context("fork")
+    t0 = time.perf_counter()
+    with ctx.Pool(cores) as pool:
+        pool.map(_cpu_worker, jobs)
+    wall = time.perf_counter() - t0
+    total = len(jobs) * nsteps
+    try:
+        model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo")
+                 if l.startswith("model name")][0]
+    except Exception:
+        model = "unknown"
+    return {"value": total / wall, "unit": "chain-leapfrog-steps/s", "cores": cores,
+            "kind": "port",
+            "sample": "%d chains x %d steps of %s geometry, NumPy port of RHMC_single_step "
+                      "(oracle/rhmc_ref.py), one chain per process, %s"
+                      % (len(jobs), nsteps, wl.name, model)}
+
+
+def load_traffic(workload):
+    """HBM bytes per launch measured by rocprofv3 PMC (profiles/pmc_<wl>.json)."""
+    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload.lower())
+    try:
+        with open(path) as fh:
+            return json.load(fh).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="C2")
+    ap.add_argument("--chains", type=int, default=None, help="chains per GPU")
+    ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    from rhmc_amd import workloads
+    wl = workloads.make(args.workload, n_chains=args.chains, seed_offset=rank)
+    # CPU baseline first: forked workers must not inherit an initialised GPU.
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline(wl)
+
+    import torch
+    import torch.distributed as dist
+    from rhmc_amd import capi
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    leap = args.leap or wl.n_steps
+    P = capi.make_params(**wl.params)
+    ctx = capi.Context(wl.D, device=local_rank)
+    q = torch.from_numpy(wl.q0).to(dev).contiguous()
+    p = torch.from_numpy(wl.p0).to(dev).contiguous()
+    it = torch.zeros((wl.n_chains, 2), dtype=torch.int32, device=dev)
+    st = torch.zeros(wl.n_chains, dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def launch():
+        ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
+                            it.data_ptr(), st.data_ptr(), stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        launch()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        launch()
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        wt = torch.tensor([wall], dtype=torch.float64)
+        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
+        wall = float(wt.item())
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+
+    stat = st.cpu().numpy()
+    nonfinite = int(((stat & capi.STATUS_NONFINITE) != 0).sum())
+
+    chain_steps = wl.n_chains * leap
+    value = chain_steps * args.steps * world / wall
+    npix = wl.D.size
+    bpu = alg_bytes_per_step(npix, wl.K)
+    achieved = bpu * chain_steps / (launch_ms * 1e-3) / 1e9
+    traffic = load_traffic(wl.name)
+    out = {
+        "metric": "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "chain-leapfrog-steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (numpy RandomState: image seed 77, chains seed 1000+rank)",
+        "config": {"workload": "%s: %dx%d image, K=%d, %d chains/GPU, %d leapfrog steps per "
+                               "launch" % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K,
+                                           wl.n_chains, leap),
+                   "chains_per_gpu": wl.n_chains, "image": list(wl.D.shape), "K": wl.K,
+                   "leapfrog_steps_per_launch": leap, "parallelism": "chain-sharded x%d" % world},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "alg_bytes_per_chain_step": bpu, "kernel_ms": launch_ms,
+                     "fp64_tflops_alg": alg_flops_per_step(npix, wl.K) * chain_steps
+                     / (launch_ms * 1e-3) / 1e12},
+        "nonfinite_chains": nonfinite,
+    }
+    if rank == 0:
+        out["cpu_baseline"] = cpu
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,813 @@
+// rhmc_kernels.hip — MI355X (gfx950) kernels of the RHMC leapfrog engine and
+// the C-ABI declared in include/rhmc.h.
+//
+// Work decomposition: one wave64 per chain; a workgroup of W waves shares the
+// data image D, staged once into LDS with coalesced loads.  After that single
+// workgroup barrier every wave runs its chain independently (only wave-local
+// LDS hand-offs), n_steps steps fused in one launch with (q, p) in registers.
+//
+// Per gradient evaluation (the inner loop, sampler_RHMC.py:365-425):
+//   * the Gaussian PSF is separable: PSF[i][j] = ex[i]*ey[j] with
+//     ex[i] = exp(-((i+.5)-x)^2/(2s^2)), ey[j] = exp(-((j+.5)-y)^2/(2s^2))/(2 pi s^2)
+//     -> (R + C) exps per star instead of R*C (utils.py:475-486);
+//   * the per-wave LDS tables hold ex, ey and the offsets (i-x)+.5, (j-y)+.5;
+//   * lane l owns pixels l, l+64, ...: Lambda = B + sum_k f_k psf_k,
+//     w_k = psf_k*(D/Lambda - 1), three running sums per star;
+//   * one butterfly all-reduce per sum.
+// The end-of-step gradient (sampler_RHMC.py:551) is evaluated at the same q
+// as the next step's first one (:525) — reflection only flips p — so it is
+// carried over: one gradient per step, bit-identical to recomputing it.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "rhmc.h"
+#include "rhmc_wave.hpp"
+
+namespace rhmc {
+
+struct Geometry {
+  int rows, cols, npix, npl;  // npl = ceil(npix / 64) pixels per lane
+  int di, dj;                 // pixel index step of 64 as (rows, cols)
+};
+
+struct Tables {  // per-wave LDS tables, K stars
+  double* ex;  // [K][rows]
+  double* dx;  // [K][rows]
+  double* ey;  // [K][cols]  (carries 1/(2 pi s^2))
+  double* dy;  // [K][cols]
+};
+
+__device__ __forceinline__ Tables carve_tables(double* base, int K, const Geometry& g) {
+  Tables t;
+  t.ex = base;
+  t.dx = base + K * g.rows;
+  t.ey = base + 2 * K * g.rows;
+  t.dy = base + 2 * K * g.rows + K * g.cols;
+  return t;
+}
+
+__host__ __device__ inline size_t table_doubles(int K, int rows, int cols) {
+  return (size_t)2 * K * (rows + cols);
+}
+
+// Build the separable PSF tables of K stars (lane k < K holds star k).
+__device__ __forceinline__ void build_tables(const Tables& t, int K, double x, double y,
+                                             const Geometry& g, const Consts& c) {
+  const int lane = lane_id();
+  const int span = g.rows + g.cols;
+  for (int k = 0; k < K; ++k) {
+    const double xk = bcast(x, k), yk = bcast(y, k);
+    for (int e = lane; e < span; e += kWave) {
+      if (e < g.rows) {
+        const double v = (e + 0.5) - xk;
+        t.ex[k * g.rows + e] = exp(-(v * v) / c.two_sig2);
+        t.dx[k * g.rows + e] = ((double)e - xk) + 0.5;
+      } else {
+        const int j = e - g.rows;
+        const double v = (j + 0.5) - yk;
+        t.ey[k * g.cols + j] = exp(-(v * v) / c.two_sig2) / c.psf_norm;
+        t.dy[k * g.cols + j] = ((double)j - yk) + 0.5;
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
+// dVdq (optionally + the dphidq metric term) for the chain of this wave.
+// Returns lane k's (g_f, g_x, g_y) for k < K; other lanes get junk.
+template <int MAXK>
+__device__ void gradient(const double* __restrict__ sD, const Tables& t, int K, double f,
+                         double x, double y, const Geometry& g, const Consts& c,
+                         bool with_metric, double& gf, double& gx, double& gy) {
+  const int lane = lane_id();
+  build_tables(t, K, x, y, g, c);
+
+  double fk[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) fk[k] = (k < K) ? bcast(f, k) : 0.0;
+
+  double acc[MAXK][3];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) acc[k][0] = acc[k][1] = acc[k][2] = 0.0;
+
+  int i = lane / g.cols, j = lane - (lane / g.cols) * g.cols;
+  for (int tt = 0; tt < g.npl; ++tt) {
+    const int pix = lane + kWave * tt;
+    if (pix < g.npix) {
+      const double dv = sD[pix];
+      double psf[MAXK];
+      double lam = c.B;  // Lambda = B + sum_k f_k PSF_k (:373-376)
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) {
+        if (k < K) {
+          psf[k] = t.ex[k * g.rows + i] * t.ey[k * g.cols + j];
+          lam = fma(fk[k], psf[k], lam);
+        }
+      }
+      const double r = dv / lam;  // rho + 1 = D/Lambda (:379)
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k) {
+        if (k < K) {
+          const double w = fma(psf[k], r, -psf[k]);  // rho * PSF
+          acc[k][0] += w;
+          acc[k][1] = fma(w, t.dx[k * g.rows + i], acc[k][1]);
+          acc[k][2] = fma(w, t.dy[k * g.cols + j], acc[k][2]);
+        }
+      }
+    }
+    j += g.dj;
+    i += g.di;
+    if (j >= g.cols) {
+      j -= g.cols;
+      ++i;
+    }
+  }
+
+  gf = gx = gy = 0.0;
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) {
+    if (k < K) {
+      const double s0 = wave_sum(acc[k][0]);
+      const double s1 = wave_sum(acc[k][1]);
+      const double s2 = wave_sum(acc[k][2]);
+      // K == 1: every lane mirrors star 0, so the chain state stays
+      // wave-uniform and the fixed-point loops never diverge.
+      if (MAXK == 1 || lane == k) {
+        gf = -s0;
+        gx = -s1 * f / c.var;
+        gy = -s2 * f / c.var;
+      }
+    }
+  }
+  if (c.use_prior) gf += c.alpha / f;  // :408-409
+  if (c.use_Vc) {                      // :411-418 (O(K^2), lanes = stars)
+    double sx = 0.0, sy = 0.0;
+    for (int jj = 0; jj < K; ++jj) {
+      const double X = bcast(x, jj), Y = bcast(y, jj);
+      const double ddx = X - x, ddy = Y - y;
+      double R = sqrt(ddx * ddx + ddy * ddy);
+      if (fabs(R) < 1e-10) R = 1e32;
+      const double tr = pow(1.0 / R, c.vc_pow + 2.0);
+      sx += tr * ddx;
+      sy += tr * ddy;
+    }
+    gx += c.beta * sx * c.vc_pow;
+    gy += c.beta * sy * c.vc_pow;
+  }
+  if (with_metric) gf += metric_flux_term(f, c);  // dphidq (:459-463)
+  // Tables are rebuilt by the next gradient call; make sure every lane has
+  // finished reading before they are overwritten.
+  wave_lds_sync();
+}
+
+struct LeapArgs {
+  double* q;
+  double* p;
+  int32_t* fp_iters;
+  int32_t* status;
+  const double* D;
+  int64_t n_chains;
+  int K, n_steps;
+  Geometry g;
+  Consts c;
+};
+
+// Stage D into LDS (coalesced, whole workgroup) and return this wave's chain.
+__device__ __forceinline__ int64_t stage_image(double* sD, const double* __restrict__ D,
+                                               int npix, int waves_per_wg) {
+  for (int e = threadIdx.x; e < npix; e += blockDim.x) sD[e] = D[e];
+  __syncthreads();
+  return (int64_t)blockIdx.x * waves_per_wg + (threadIdx.x / kWave);
+}
+
+// n_steps implicit generalized-leapfrog steps (sampler_RHMC.py:522-566).
+template <int MAXK>
+__global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
+  extern __shared__ double lds[];
+  const Geometry& g = a.g;
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  double* sD = lds;
+  const int64_t chain = stage_image(sD, a.D, g.npix, W);
+  if (chain >= a.n_chains) return;
+  const int lane = lane_id();
+  const int K = a.K;
+  const Tables tab = carve_tables(lds + g.npix + (threadIdx.x / kWave) * table_doubles(K, g.rows, g.cols), K, g);
+
+  // lane k < K owns star k
+  const bool owner = lane < K;
+  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+
+  int it_p = 0, it_q = 0;
+  unsigned st = 0u;
+  const double hdt = c.hdt;
+  double gf, gx, gy;
+  gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
+
+  for (int s = 0; s < a.n_steps; ++s) {
+    // (1) half kick with dphidq (:525)
+    pf = pf - hdt * gf;
+    px = px - hdt * gx;
+    py = py - hdt * gy;
+
+    // (2) p fixed point, flux slots only (:528-535); x/y slots change by 0
+    {
+      const double coef = dtaudq_coef(f, c);
+      const double rho = pf;
+      double dp;
+      int n = 0;
+      do {
+        const double pp = rho - hdt * ((pf * pf) * coef / 2.0);
+        double d = (MAXK == 1 || owner) ? fabs(pf - pp) : 0.0;
+        dp = (MAXK == 1) ? d : wave_nanmax(d);
+        pf = pp;
+        ++n;
+      } while (dp > c.delta && n < c.counter_max);
+      it_p += n;
+      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
+    }
+
+    // (3) q fixed point (:538-545): q' = sig + dt/2 (p/H(sig) + p/H(q))
+    {
+      const double sf = f, sx = x, sy = y;
+      const double hff0 = H_ff(sf, c), hxx0 = H_xx(sf, c);
+      const double af = pf / hff0, ax = px / hxx0, ay = py / hxx0;
+      double dq;
+      int n = 0;
+      do {
+        const double hff = H_ff(f, c), hxx = H_xx(f, c);
+        const double nf = sf + hdt * (af + pf / hff);
+        const double nx = sx + hdt * (ax + px / hxx);
+        const double ny = sy + hdt * (ay + py / hxx);
+        double d = nanmax2(nanmax2(fabs(f - nf), fabs(x - nx)), fabs(y - ny));
+        d = (MAXK == 1 || owner) ? d : 0.0;
+        dq = (MAXK == 1) ? d : wave_nanmax(d);
+        f = nf;
+        x = nx;
+        y = ny;
+        ++n;
+      } while (dq > c.delta && n < c.counter_max);
+      it_q += n;
+      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
+    }
+
+    // (4) p -= dt/2 dtaudq(q, p) (:548)
+    pf = pf - hdt * ((pf * pf) * dtaudq_coef(f, c) / 2.0);
+
+    // (5) p -= dt/2 dphidq(q) (:551); the gradient carries to the next step
+    gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
+    pf = pf - hdt * gf;
+    px = px - hdt * gx;
+    py = py - hdt * gy;
+
+    // (6) flux wall and edge reflection (:554-564)
+    if (f < c.f_lim) {
+      pf = -pf;
+      st |= RHMC_STATUS_REFLECT_F;
+    }
+    if (x < 0.0 || x > (double)(g.rows - 1)) {
+      px = -px;
+      st |= RHMC_STATUS_REFLECT_XY;
+    }
+    if (y < 0.0 || y > (double)(g.cols - 1)) {
+      py = -py;
+      st |= RHMC_STATUS_REFLECT_XY;
+    }
+  }
+
+  if (owner) {
+    if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
+          isfinite(py)))
+      st |= RHMC_STATUS_NONFINITE;
+    a.q[base] = f;
+    a.q[base + 1] = x;
+    a.q[base + 2] = y;
+    a.p[base] = pf;
+    a.p[base + 1] = px;
+    a.p[base + 2] = py;
+  }
+  // OR the star lanes' status bits (only lanes < K set reflection bits)
+  unsigned all = owner ? st : 0u;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) all |= (unsigned)__shfl_xor((int)all, m, kWave);
+  if (lane == 0) {
+    if (a.status) a.status[chain] = (int32_t)all;
+    if (a.fp_iters) {
+      a.fp_iters[2 * chain] = it_p;
+      a.fp_iters[2 * chain + 1] = it_q;
+    }
+  }
+}
+
+struct GradArgs {
+  const double* q;
+  double* grad;
+  const double* D;
+  int64_t n_chains;
+  int K, with_metric;
+  Geometry g;
+  Consts c;
+};
+
+template <int MAXK>
+__global__ void __launch_bounds__(256) gradient_kernel(GradArgs a) {
+  extern __shared__ double lds[];
+  const int W = blockDim.x / kWave;
+  const int64_t chain = stage_image(lds, a.D, a.g.npix, W);
+  if (chain >= a.n_chains) return;
+  const int lane = lane_id();
+  const int K = a.K;
+  const Tables tab = carve_tables(lds + a.g.npix + (threadIdx.x / kWave) * table_doubles(K, a.g.rows, a.g.cols), K, a.g);
+  const bool owner = lane < K;
+  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double gf, gx, gy;
+  gradient<MAXK>(lds, tab, K, f, x, y, a.g, a.c, a.with_metric != 0, gf, gx, gy);
+  if (owner) {
+    a.grad[base] = gf;
+    a.grad[base + 1] = gx;
+    a.grad[base + 2] = gy;
+  }
+}
+
+struct EnergyArgs {
+  const double* q;
+  const double* p;
+  double* V;
+  double* T;
+  const double* D;
+  int64_t n_chains;
+  int K, f_pos;
+  Geometry g;
+  Consts c;
+};
+
+// V (sampler_RHMC.py:294-351) and T at H(q) (:353-363), one wave per chain.
+template <int MAXK>
+__global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
+  extern __shared__ double lds[];
+  const Geometry& g = a.g;
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  const int64_t chain = stage_image(lds, a.D, g.npix, W);
+  if (chain >= a.n_chains) return;
+  const int lane = lane_id();
+  const int K = a.K;
+  const Tables tab = carve_tables(lds + g.npix + (threadIdx.x / kWave) * table_doubles(K, g.rows, g.cols), K, g);
+  const bool owner = lane < K;
+  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+
+  if (a.T) {
+    double t1 = 0.0, t2 = 0.0;
+    if (owner) {
+      const double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+      const double hff = H_ff(f, c), hxx = H_xx(f, c);
+      t1 = pf * pf / hff + px * px / hxx + py * py / hxx;
+      t2 = log(fabs(hff)) + log(fabs(hxx)) + log(fabs(hxx));
+    }
+    t1 = wave_sum(t1);
+    t2 = wave_sum(t2);
+    if (lane == 0) a.T[chain] = (t1 + t2) / 2.0;
+  }
+  if (!a.V) return;
+
+  // Infinite potential outside the support (:303-317)
+  bool bad = false;
+  if (owner) {
+    if (a.f_pos && f < c.f_lim) bad = true;
+    if (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)) bad = true;
+  }
+  if (__any(bad)) {
+    if (lane == 0) a.V[chain] = INFINITY;
+    return;
+  }
+
+  build_tables(tab, K, x, y, g, c);
+  double fk[MAXK];
+#pragma unroll
+  for (int k = 0; k < MAXK; ++k) fk[k] = (k < K) ? bcast(f, k) : 0.0;
+  double v = 0.0;
+  int i = lane / g.cols, j = lane - (lane / g.cols) * g.cols;
+  for (int tt = 0; tt < g.npl; ++tt) {
+    const int pix = lane + kWave * tt;
+    if (pix < g.npix) {
+      double lam = c.B;
+#pragma unroll
+      for (int k = 0; k < MAXK; ++k)
+        if (k < K) lam = fma(fk[k], tab.ex[k * g.rows + i] * tab.ey[k * g.cols + j], lam);
+      v += lam - lds[pix] * log(lam);
+    }
+    j += g.dj;
+    i += g.di;
+    if (j >= g.cols) {
+      j -= g.cols;
+      ++i;
+    }
+  }
+  v = wave_sum(v);
+  if (c.use_prior) {  // V_prior accumulated per star, added after the sum (:326, :329-330)
+    const double vp = wave_sum(owner ? c.alpha * log(f) + c.vprior : 0.0);
+    v += vp;
+  }
+  if (c.use_Vc) {  // 0.5 beta sum_{a,b} R_ab^-pow with R_aa -> 1e32 (:332-349)
+    double s = 0.0;
+    for (int jj = 0; jj < K; ++jj) {
+      const double X = bcast(x, jj), Y = bcast(y, jj);
+      double R = sqrt((X - x) * (X - x) + (Y - y) * (Y - y));
+      if (fabs(R) < 1e-10) R = 1e32;
+      s += pow(1.0 / R, c.vc_pow);
+    }
+    v += 0.5 * c.beta * wave_sum(owner ? s : 0.0);
+  }
+  if (lane == 0) a.V[chain] = v;
+}
+
+}  // namespace rhmc
+
+// ============================================================================
+// Host side: C-ABI
+// ============================================================================
+using namespace rhmc;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                               \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess)                                                           \
+      return fail(RHMC_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct rhmc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int rows = 0, cols = 0;
+  double* d_D = nullptr;
+  // scratch for the host-pointer entry points
+  void* scratch = nullptr;
+  size_t scratch_bytes = 0;
+  int max_lds = 0;
+};
+
+namespace {
+
+constexpr int kMaxKSupported = 16;
+
+Geometry make_geometry(int rows, int cols) {
+  Geometry g;
+  g.rows = rows;
+  g.cols = cols;
+  g.npix = rows * cols;
+  g.npl = (g.npix + kWave - 1) / kWave;
+  g.di = kWave / cols;
+  g.dj = kWave % cols;
+  return g;
+}
+
+int make_consts(const rhmc_params* P, Consts* c) {
+  if (!P) return fail(RHMC_ERR_ARG, "params is NULL");
+  if (P->reserved != 0) return fail(RHMC_ERR_ARG, "params.reserved must be 0");
+  std::memset(c, 0, sizeof(*c));
+  c->dt = P->dt;
+  c->hdt = P->dt / 2.0;
+  c->delta = P->delta;
+  c->B = P->B_count;
+  c->f_lim = P->f_lim;
+  c->f_low = P->f_low;
+  const double sigma = P->fwhm_pix / 2.354;  // utils.py:480
+  c->two_sig2 = 2 * (sigma * sigma);         // 2*sigma**2 (:484)
+  c->psf_norm = (M_PI * 2) * (sigma * sigma);
+  const double sv = P->fwhm_pix / 2.354;
+  c->var = sv * sv;  // (PSF_FWHM_pix/2.354)**2 (sampler_RHMC.py:384)
+  c->g_xx = P->g_xx;
+  c->g_ff = P->g_ff;
+  c->g_ff2 = P->g_ff2;
+  c->g0 = P->g0;
+  c->g1 = P->g1;
+  c->g2 = P->g2;
+  c->c0 = (P->B_count / P->g0) / P->g_ff;
+  c->alpha = P->alpha;
+  c->beta = P->beta;
+  c->vc_pow = P->Vc_r_pow;
+  c->vprior = P->V_prior_const;
+  c->counter_max = P->counter_max;
+  c->use_prior = P->use_prior != 0;
+  c->use_Vc = P->use_Vc != 0;
+  return RHMC_OK;
+}
+
+// Workgroup shape: W waves share one LDS copy of D; pick the largest W<=4
+// whose LDS fits.
+int pick_waves(const rhmc_ctx* ctx, int K, size_t* lds_bytes, int* W_out) {
+  const size_t img = (size_t)ctx->rows * ctx->cols * sizeof(double);
+  const size_t tab = table_doubles(K, ctx->rows, ctx->cols) * sizeof(double);
+  for (int W = 4; W >= 1; W >>= 1) {
+    const size_t need = img + W * tab;
+    if (need <= (size_t)ctx->max_lds) {
+      *lds_bytes = need;
+      *W_out = W;
+      return RHMC_OK;
+    }
+  }
+  return fail(RHMC_ERR_UNSUPPORTED,
+              "image + PSF tables exceed LDS (" + std::to_string(img + tab) + " B > " +
+                  std::to_string(ctx->max_lds) + " B); large images are not built yet");
+}
+
+int check_common(rhmc_ctx* ctx, int64_t n_chains, int32_t K) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
+  if (n_chains < 0) return fail(RHMC_ERR_ARG, "n_chains < 0");
+  if (K < 1 || K > 64) return fail(RHMC_ERR_ARG, "K must be in [1, 64]");
+  if (K > kMaxKSupported)
+    return fail(RHMC_ERR_UNSUPPORTED, "K > " + std::to_string(kMaxKSupported) + " not built yet");
+  if (n_chains > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "n_chains too large");
+  return RHMC_OK;
+}
+
+int ensure_scratch(rhmc_ctx* ctx, size_t bytes) {
+  if (bytes <= ctx->scratch_bytes) return RHMC_OK;
+  if (ctx->scratch) HIP_TRY(hipFree(ctx->scratch));
+  ctx->scratch = nullptr;
+  ctx->scratch_bytes = 0;
+  if (hipMalloc(&ctx->scratch, bytes) != hipSuccess)
+    return fail(RHMC_ERR_NOMEM, "hipMalloc scratch " + std::to_string(bytes) + " B failed");
+  ctx->scratch_bytes = bytes;
+  return RHMC_OK;
+}
+
+template <template <int> class Launcher, typename Args>
+int dispatch_k(int K, dim3 grid, dim3 block, size_t lds, hipStream_t s, const Args& a) {
+  if (K == 1) return Launcher<1>::go(grid, block, lds, s, a);
+  if (K <= 2) return Launcher<2>::go(grid, block, lds, s, a);
+  if (K <= 4) return Launcher<4>::go(grid, block, lds, s, a);
+  if (K <= 8) return Launcher<8>::go(grid, block, lds, s, a);
+  return Launcher<16>::go(grid, block, lds, s, a);
+}
+
+template <int MAXK>
+struct LeapLaunch {
+  static int go(dim3 grid, dim3 block, size_t lds, hipStream_t s, const LeapArgs& a) {
+    hipLaunchKernelGGL(leapfrog_kernel<MAXK>, grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return RHMC_OK;
+  }
+};
+template <int MAXK>
+struct GradLaunch {
+  static int go(dim3 grid, dim3 block, size_t lds, hipStream_t s, const GradArgs& a) {
+    hipLaunchKernelGGL(gradient_kernel<MAXK>, grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return RHMC_OK;
+  }
+};
+template <int MAXK>
+struct EnergyLaunch {
+  static int go(dim3 grid, dim3 block, size_t lds, hipStream_t s, const EnergyArgs& a) {
+    hipLaunchKernelGGL(energy_kernel<MAXK>, grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return RHMC_OK;
+  }
+};
+
+int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                    int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
+                    hipStream_t s) {
+  LeapArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
+  if (P->counter_max < 1) return fail(RHMC_ERR_ARG, "counter_max < 1");
+  if (n_chains == 0) return RHMC_OK;
+  size_t lds;
+  int W;
+  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
+  a.q = d_q;
+  a.p = d_p;
+  a.fp_iters = d_it;
+  a.status = d_st;
+  a.D = ctx->d_D;
+  a.n_chains = n_chains;
+  a.K = K;
+  a.n_steps = n_steps;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
+  return dispatch_k<LeapLaunch>(K, grid, block, lds, s, a);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rhmc_abi_version(void) { return RHMC_ABI_VERSION; }
+
+const char* rhmc_last_error(void) { return g_err.c_str(); }
+
+int rhmc_device_count(int* n) {
+  if (!n) return fail(RHMC_ERR_ARG, "n is NULL");
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  *n = (e == hipSuccess) ? c : 0;
+  return RHMC_OK;
+}
+
+int rhmc_ctx_set_image(rhmc_ctx* ctx, const double* D, int32_t rows, int32_t cols) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!D) return fail(RHMC_ERR_ARG, "D is NULL");
+  if (rows < 1 || cols < 1) return fail(RHMC_ERR_ARG, "rows/cols must be >= 1");
+  if (rows != cols)
+    return fail(RHMC_ERR_ARG, "rows must equal cols (reference gauss_PSF is square-only)");
+  if ((int64_t)rows * cols > (1 << 26)) return fail(RHMC_ERR_ARG, "image too large");
+  HIP_TRY(hipSetDevice(ctx->device));
+  const size_t bytes = (size_t)rows * cols * sizeof(double);
+  if (ctx->d_D && (ctx->rows * ctx->cols != rows * cols)) {
+    HIP_TRY(hipFree(ctx->d_D));
+    ctx->d_D = nullptr;
+  }
+  if (!ctx->d_D && hipMalloc(&ctx->d_D, bytes) != hipSuccess)
+    return fail(RHMC_ERR_NOMEM, "hipMalloc image failed");
+  HIP_TRY(hipMemcpyAsync(ctx->d_D, D, bytes, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->rows = rows;
+  ctx->cols = cols;
+  return RHMC_OK;
+}
+
+int rhmc_ctx_create(int device, const double* D, int32_t rows, int32_t cols, rhmc_ctx** out) {
+  if (!out) return fail(RHMC_ERR_ARG, "out is NULL");
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(RHMC_ERR_HIP, "no HIP device");
+  if (device < 0 || device >= n) return fail(RHMC_ERR_ARG, "device out of range");
+  HIP_TRY(hipSetDevice(device));
+  rhmc_ctx* ctx = new rhmc_ctx();
+  ctx->device = device;
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    delete ctx;
+    return fail(RHMC_ERR_HIP, "hipGetDeviceProperties failed");
+  }
+  ctx->max_lds = (int)prop.sharedMemPerBlock;
+  if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return fail(RHMC_ERR_HIP, "hipStreamCreate failed");
+  }
+  int rc = rhmc_ctx_set_image(ctx, D, rows, cols);
+  if (rc) {
+    std::string keep = g_err;
+    rhmc_ctx_destroy(ctx);
+    g_err = keep;
+    return rc;
+  }
+  *out = ctx;
+  return RHMC_OK;
+}
+
+int rhmc_ctx_image_device(rhmc_ctx* ctx, const double** d_image) {
+  if (!ctx || !d_image) return fail(RHMC_ERR_ARG, "NULL argument");
+  *d_image = ctx->d_D;
+  return RHMC_OK;
+}
+
+void rhmc_ctx_destroy(rhmc_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->d_D) (void)hipFree(ctx->d_D);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+int rhmc_ctx_synchronize(rhmc_ctx* ctx) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  HIP_TRY(hipSetDevice(ctx->device));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                         int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_fp_iters,
+                         int32_t* d_status, void* stream) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains > 0 && (!d_q || !d_p)) return fail(RHMC_ERR_ARG, "q/p is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_leapfrog(ctx, P, d_q, d_p, n_chains, K, n_steps, d_fp_iters, d_status, s);
+}
+
+int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p, int64_t n_chains,
+                  int32_t K, int32_t n_steps, int32_t* fp_iters, int32_t* status) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0) return RHMC_OK;
+  if (!q || !p) return fail(RHMC_ERR_ARG, "q/p is NULL");
+  const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
+  const size_t ib = (size_t)n_chains * 2 * sizeof(int32_t);
+  const size_t tb = (size_t)n_chains * sizeof(int32_t);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, 2 * sb + ib + tb + 256))) return rc;
+  char* base = (char*)ctx->scratch;
+  double* dq = (double*)base;
+  double* dp = (double*)(base + sb);
+  int32_t* dit = (int32_t*)(base + 2 * sb);
+  int32_t* dst = (int32_t*)(base + 2 * sb + ib);
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = launch_leapfrog(ctx, P, dq, dp, n_chains, K, n_steps, dit, dst, ctx->stream)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(p, dp, sb, hipMemcpyDeviceToHost, ctx->stream));
+  if (fp_iters) HIP_TRY(hipMemcpyAsync(fp_iters, dit, ib, hipMemcpyDeviceToHost, ctx->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(status, dst, tb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* grad,
+                  int64_t n_chains, int32_t K, int32_t kind) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (kind != 0 && kind != 1) return fail(RHMC_ERR_ARG, "kind must be 0 (dVdq) or 1 (dphidq)");
+  if (n_chains == 0) return RHMC_OK;
+  if (!q || !grad) return fail(RHMC_ERR_ARG, "q/grad is NULL");
+  GradArgs a;
+  if ((rc = make_consts(P, &a.c))) return rc;
+  size_t lds;
+  int W;
+  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
+  const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, 2 * sb + 256))) return rc;
+  double* dq = (double*)ctx->scratch;
+  double* dg = (double*)((char*)ctx->scratch + sb);
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  a.q = dq;
+  a.grad = dg;
+  a.D = ctx->d_D;
+  a.n_chains = n_chains;
+  a.K = K;
+  a.with_metric = kind;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
+  if ((rc = dispatch_k<GradLaunch>(K, grid, block, lds, ctx->stream, a))) return rc;
+  HIP_TRY(hipMemcpyAsync(grad, dg, sb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const double* p, double* V,
+                double* T, int64_t n_chains, int32_t K, int32_t f_pos) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0) return RHMC_OK;
+  if (!q) return fail(RHMC_ERR_ARG, "q is NULL");
+  if (T && !p) return fail(RHMC_ERR_ARG, "T requested but p is NULL");
+  EnergyArgs a;
+  if ((rc = make_consts(P, &a.c))) return rc;
+  size_t lds;
+  int W;
+  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
+  const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
+  const size_t eb = (size_t)n_chains * sizeof(double);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, 2 * sb + 2 * eb + 256))) return rc;
+  char* base = (char*)ctx->scratch;
+  double* dq = (double*)base;
+  double* dp = (double*)(base + sb);
+  double* dV = (double*)(base + 2 * sb);
+  double* dT = (double*)(base + 2 * sb + eb);
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  if (T) HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
+  a.q = dq;
+  a.p = T ? dp : nullptr;
+  a.V = V ? dV : nullptr;
+  a.T = T ? dT : nullptr;
+  a.D = ctx->d_D;
+  a.n_chains = n_chains;
+  a.K = K;
+  a.f_pos = f_pos != 0;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
+  if ((rc = dispatch_k<EnergyLaunch>(K, grid, block, lds, ctx->stream, a))) return rc;
+  if (V) HIP_TRY(hipMemcpyAsync(V, dV, eb, hipMemcpyDeviceToHost, ctx->stream));
+  if (T) HIP_TRY(hipMemcpyAsync(T, dT, eb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// rhmc_wave.hpp — wave64 building blocks and the per-star metric of the RHMC
+// step, written for gfx950 (CDNA4).  One wavefront owns one chain; lane k < K
+// owns star k's (f, x, y) and (p_f, p_x, p_y).
+//
+// Reference formulas (file:line into jaekor91/HMC-stellar-toy-model):
+//   H_ff  sampler_RHMC.py:283-292   H_xx sampler_RHMC.py:260-280
+//   dphidq metric term :459-463     dtaudq :467-483     dtaudp :485-492
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rhmc {
+
+constexpr int kWave = 64;
+
+// Constants derived on the host from rhmc_params exactly the way the reference
+// derives them (sigma = FWHM/2.354, 2*sigma**2, pi*2*sigma**2, var, (B/g0)/g_ff).
+struct Consts {
+  double dt, hdt, delta;
+  double B, f_lim, f_low;
+  double two_sig2, psf_norm, var;
+  double g_xx, g_ff, g_ff2, g0, g1, g2, c0;
+  double alpha, beta, vc_pow, vprior;
+  int counter_max, use_prior, use_Vc, pad;
+};
+
+// ---------------------------------------------------------------- lane moves
+__device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+
+// Broadcast lane `src` (wave-uniform) of a double to every lane: two
+// v_readlane_b32 into SGPRs, no LDS traffic.
+__device__ __forceinline__ double bcast(double v, int src) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, src);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), src);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Butterfly all-reduce; every lane ends with the same, deterministic sum.
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m, kWave);
+  return v;
+}
+
+// NaN-propagating max, matching np.max on an array holding a NaN.
+__device__ __forceinline__ double nanmax2(double a, double b) {
+  return (a != a || a > b) ? a : b;
+}
+__device__ __forceinline__ double wave_nanmax(double v) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) v = nanmax2(v, __shfl_xor(v, m, kWave));
+  return v;
+}
+
+// Wave-local LDS hand-off (tables written by some lanes, read by others).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// ------------------------------------------------------------ per-star metric
+// H_ff(f) = 1/(f/g_ff2 + (B/g0)/g_ff)                       (:290)
+__device__ __forceinline__ double H_ff(double f, const Consts& c) {
+  return 1.0 / (f / c.g_ff2 + c.c0);
+}
+// dH_ff/df as the reference writes it: -1/(f + (B/g0)/g_ff)**2 — ignores
+// g_ff2, the true derivative only when g_ff2 == 1 (quirk kept, :292).
+__device__ __forceinline__ double H_ff_grad(double f, const Consts& c) {
+  const double t = f + c.c0;
+  return -1.0 / (t * t);
+}
+// H_xx(f) = g_xx / (1/(g1 f) + B/(g2 f^2)), f clamped to f_low (:267-273).
+__device__ __forceinline__ double H_xx_s(double f, const Consts& c) {
+  return 1.0 / (c.g1 * f) + c.B / (c.g2 * (f * f));
+}
+__device__ __forceinline__ double H_xx(double f, const Consts& c) {
+  const double fl = (f < c.f_low) ? c.f_low : f;
+  return c.g_xx * (1.0 / H_xx_s(fl, c));
+}
+// dH_xx/df, 0 when clamped (:275-278).
+__device__ __forceinline__ double H_xx_grad(double f, const Consts& c) {
+  if (f < c.f_low) return 0.0;
+  const double s = H_xx_s(f, c);
+  const double a = 1.0 / (c.g1 * (f * f)) + 2.0 * c.B / (c.g2 * (f * f * f));
+  return c.g_xx * a * (1.0 / (s * s));
+}
+
+// dphidq's metric term on the flux slot: (H_ff'/H_ff + 2 H_xx'/H_xx)/2 (:461-463)
+__device__ __forceinline__ double metric_flux_term(double f, const Consts& c) {
+  const double hff = H_ff(f, c), hffg = H_ff_grad(f, c);
+  const double hxx = H_xx(f, c), hxxg = H_xx_grad(f, c);
+  return ((hffg / hff) + (2.0 * hxxg / hxx)) / 2.0;
+}
+
+// dtaudq on the flux slot: (p_f^2 * (-H_ff'/H_ff^2))/2 — x, y slots are 0 (:479-481).
+// `coef` = -H_ff'/H_ff^2 is constant while q is fixed (the whole p-loop).
+__device__ __forceinline__ double dtaudq_coef(double f, const Consts& c) {
+  const double h = H_ff(f, c);
+  return -H_ff_grad(f, c) / (h * h);
+}
+
+}  // namespace rhmc

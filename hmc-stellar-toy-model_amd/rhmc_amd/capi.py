@@ -1,0 +1,248 @@
+"""ctypes binding of librhmc.so (include/rhmc.h).
+
+Thin by design: argument marshalling, shape checks and error translation.
+The library is REQUIRED — there is no CPU fallback; importing this module
+without a built librhmc.so raises.  On a machine without a GPU the library
+still loads (so its exports can be checked) but every compute entry point
+returns an error.
+"""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+_PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.environ.get("RHMC_LIB", os.path.join(_PKG_DIR, "librhmc.so"))
+
+RHMC_OK = 0
+RHMC_ERR_ARG = -1
+RHMC_ERR_HIP = -2
+RHMC_ERR_NOMEM = -3
+RHMC_ERR_UNSUPPORTED = -4
+
+STATUS_NONFINITE = 1
+STATUS_PLOOP_CAP = 2
+STATUS_QLOOP_CAP = 4
+STATUS_REFLECT_F = 8
+STATUS_REFLECT_XY = 16
+
+EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
+           "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
+           "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
+           "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy")
+
+
+class RhmcParams(ctypes.Structure):
+    """Mirror of `rhmc_params` (include/rhmc.h)."""
+    _fields_ = [
+        ("dt", ctypes.c_double), ("delta", ctypes.c_double),
+        ("B_count", ctypes.c_double), ("f_lim", ctypes.c_double),
+        ("f_low", ctypes.c_double), ("fwhm_pix", ctypes.c_double),
+        ("g_xx", ctypes.c_double), ("g_ff", ctypes.c_double),
+        ("g_ff2", ctypes.c_double), ("g0", ctypes.c_double),
+        ("g1", ctypes.c_double), ("g2", ctypes.c_double),
+        ("alpha", ctypes.c_double), ("beta", ctypes.c_double),
+        ("Vc_r_pow", ctypes.c_double), ("V_prior_const", ctypes.c_double),
+        ("counter_max", ctypes.c_int32), ("use_prior", ctypes.c_int32),
+        ("use_Vc", ctypes.c_int32), ("reserved", ctypes.c_int32),
+    ]
+
+
+class RhmcError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("librhmc error %d: %s" % (code, msg))
+        self.code = code
+
+
+def _load():
+    if "torch" in sys.modules or os.environ.get("RHMC_IMPORT_TORCH") == "1":
+        # Bind to the HIP runtime torch already loaded (same soname), so device
+        # pointers and streams from torch are valid here.
+        import torch  # noqa: F401
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("librhmc.so not built at %s — run __graft_entry__.build()" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    P = ctypes.POINTER
+    c_dp = P(ctypes.c_double)
+    c_ip = P(ctypes.c_int32)
+    vp = ctypes.c_void_p
+    sig = {
+        "rhmc_abi_version": (ctypes.c_int, []),
+        "rhmc_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "rhmc_last_error": (ctypes.c_char_p, []),
+        "rhmc_ctx_create": (ctypes.c_int, [ctypes.c_int, c_dp, ctypes.c_int32, ctypes.c_int32, P(vp)]),
+        "rhmc_ctx_set_image": (ctypes.c_int, [vp, c_dp, ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_ctx_image_device": (ctypes.c_int, [vp, P(vp)]),
+        "rhmc_ctx_destroy": (None, [vp]),
+        "rhmc_ctx_synchronize": (ctypes.c_int, [vp]),
+        "rhmc_leapfrog": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, ctypes.c_int64,
+                                         ctypes.c_int32, ctypes.c_int32, c_ip, c_ip]),
+        "rhmc_leapfrog_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, ctypes.c_int64,
+                                                ctypes.c_int32, ctypes.c_int32, vp, vp, vp]),
+        "rhmc_gradient": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, ctypes.c_int64,
+                                         ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_energy": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_dp,
+                                       ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+def abi_version():
+    return _lib.rhmc_abi_version()
+
+
+def device_count():
+    n = ctypes.c_int(0)
+    _lib.rhmc_device_count(ctypes.byref(n))
+    return n.value
+
+
+def device_available():
+    return device_count() > 0
+
+
+def _check(rc):
+    if rc != RHMC_OK:
+        raise RhmcError(rc, _lib.rhmc_last_error().decode(errors="replace"))
+
+
+def _dptr(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _iptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _f64(a, name):
+    a = np.asarray(a)
+    if a.dtype != np.float64:
+        raise TypeError("%s must be float64, got %s" % (name, a.dtype))
+    return np.ascontiguousarray(a)
+
+
+def make_params(dt, delta, counter_max, B_count, f_lim, f_low, fwhm_pix, g_xx, g_ff,
+                g_ff2, g0, g1, g2, use_prior=False, alpha=2., use_Vc=False, beta=1.,
+                Vc_r_pow=1., V_prior_const=0.):
+    return RhmcParams(float(dt), float(delta), float(B_count), float(f_lim), float(f_low),
+                      float(fwhm_pix), float(g_xx), float(g_ff), float(g_ff2), float(g0),
+                      float(g1), float(g2), float(alpha), float(beta), float(Vc_r_pow),
+                      float(V_prior_const), int(counter_max), int(bool(use_prior)),
+                      int(bool(use_Vc)), 0)
+
+
+class Context:
+    """One GPU + one data image (rhmc_ctx)."""
+
+    def __init__(self, D, device=0):
+        D = _f64(D, "D")
+        if D.ndim != 2:
+            raise ValueError("D must be 2-D")
+        h = ctypes.c_void_p()
+        _check(_lib.rhmc_ctx_create(int(device), _dptr(D), D.shape[0], D.shape[1],
+                                    ctypes.byref(h)))
+        self._h = h
+        self.shape = D.shape
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_image(self, D):
+        D = _f64(D, "D")
+        _check(_lib.rhmc_ctx_set_image(self._h, _dptr(D), D.shape[0], D.shape[1]))
+        self.shape = D.shape
+
+    def image_device_ptr(self):
+        p = ctypes.c_void_p()
+        _check(_lib.rhmc_ctx_image_device(self._h, ctypes.byref(p)))
+        return p.value
+
+    def synchronize(self):
+        _check(_lib.rhmc_ctx_synchronize(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.rhmc_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- compute ----------------------------------------------------------
+    def leapfrog(self, params, q, p, n_steps, K=None, return_info=False):
+        """n_steps fused RHMC_single_step()s; q, p: [n_chains, 3K] (or [3K]).
+        Returns new (q, p) arrays (inputs are not mutated, like the reference)."""
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        p2 = np.array(p, dtype=np.float64, order="C", copy=True)
+        if q2.shape != p2.shape:
+            raise ValueError("q and p shapes differ")
+        single = q2.ndim == 1
+        q2 = q2.reshape(-1, q2.shape[-1]) if not single else q2.reshape(1, -1)
+        p2 = p2.reshape(q2.shape)
+        if q2.shape[1] % 3:
+            raise ValueError("last dimension must be 3K")
+        K = q2.shape[1] // 3 if K is None else K
+        n = q2.shape[0]
+        it = np.zeros((n, 2), np.int32)
+        st = np.zeros(n, np.int32)
+        _check(_lib.rhmc_leapfrog(self._h, ctypes.byref(params), _dptr(q2), _dptr(p2), n,
+                                  int(K), int(n_steps), _iptr(it), _iptr(st)))
+        if single:
+            q2, p2, it, st = q2[0], p2[0], it[0], st[0]
+        if return_info:
+            return q2, p2, it, st
+        return q2, p2
+
+    def leapfrog_device(self, params, q_ptr, p_ptr, n_chains, K, n_steps, iters_ptr=None,
+                        status_ptr=None, stream=None):
+        _check(_lib.rhmc_leapfrog_device(self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr),
+                                         ctypes.c_void_p(p_ptr), int(n_chains), int(K),
+                                         int(n_steps), ctypes.c_void_p(iters_ptr or 0),
+                                         ctypes.c_void_p(status_ptr or 0),
+                                         ctypes.c_void_p(stream or 0)))
+
+    def gradient(self, params, q, kind=0):
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        single = q2.ndim == 1
+        q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
+        g = np.empty_like(q2)
+        _check(_lib.rhmc_gradient(self._h, ctypes.byref(params), _dptr(q2), _dptr(g),
+                                  q2.shape[0], q2.shape[1] // 3, int(kind)))
+        return g[0] if single else g
+
+    def energy(self, params, q, p=None, f_pos=False):
+        """Returns (V, T); T is None when p is None."""
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        single = q2.ndim == 1
+        q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
+        n = q2.shape[0]
+        V = np.empty(n)
+        T = None
+        pp = None
+        if p is not None:
+            pp = np.array(p, dtype=np.float64, order="C", copy=True).reshape(q2.shape)
+            T = np.empty(n)
+        _check(_lib.rhmc_energy(self._h, ctypes.byref(params), _dptr(q2),
+                                None if pp is None else _dptr(pp), _dptr(V),
+                                None if T is None else _dptr(T), n, q2.shape[1] // 3,
+                                int(bool(f_pos))))
+        if single:
+            return V[0], (None if T is None else T[0])
+        return V, T

@@ -1,0 +1,102 @@
+"""Synthetic workloads of BASELINE.json's configs.
+
+Every config is a data image plus a batch of chain states (q0, p0):
+  C1  32x32,  K=1,  1 chain,        100 steps (reference CPU plumbing case)
+  C2  48x48,  K=1,  4096 chains,    500 steps (headline, one MI355X)
+  C3  48x48,  K=10, 16384 chains    (multi-source gradient)
+  C4  48x48,  K=1,  2^20 chains     sharded over 8 GPUs
+  C5  256x256, K=64, 8192 chains    (flux-wall RHMC, prior on)
+
+Randomness: numpy legacy RandomState; the image uses seed 77
+(RHMC-big-sim4.py:18), chain initial states seed 1000 (+ shard offset).
+"""
+import numpy as np
+
+from .photometry import (default_exp_setup, factors, gauss_PSF, gen_pow_law_sample,
+                         mag2flux, metric_diag, poisson_realization)
+
+
+class Workload:
+    def __init__(self, name, D, q0, p0, params, n_steps, K, note):
+        self.name = name
+        self.D = D
+        self.q0 = q0
+        self.p0 = p0
+        self.params = params        # dict for capi.make_params
+        self.n_steps = n_steps
+        self.K = K
+        self.note = note
+
+    @property
+    def n_chains(self):
+        return self.q0.shape[0]
+
+
+def base_params(dt, g_xx=1., g_ff=1., g_ff2=1., use_prior=False, alpha=2.):
+    """Instance constants of multi_gym(g_xx, g_ff, g_ff2) with the factors
+    computed once on the default 48x48 grid (sampler_RHMC.py:50, :165)."""
+    rows, cols, ftc, fwhm, B, _, mB, f_lim = default_exp_setup()
+    g0, g1, g2 = factors(rows, cols, rows / 2., cols / 2., fwhm)
+    return dict(dt=dt, delta=1e-6, counter_max=1000, B_count=B, f_lim=f_lim,
+                f_low=mag2flux(mB + 2) * ftc, fwhm_pix=fwhm, g_xx=g_xx, g_ff=g_ff,
+                g_ff2=g_ff2, g0=g0, g1=g1, g2=g2, use_prior=use_prior, alpha=alpha,
+                use_Vc=False, beta=1., Vc_r_pow=1., V_prior_const=0.), ftc
+
+
+def _image(n, stars, ftc, B, fwhm, rng):
+    D0 = np.ones((n, n)) * B
+    for mag, x, y in stars:
+        D0 += mag2flux(mag) * ftc * gauss_PSF(n, n, x, y, FWHM=fwhm)
+    return poisson_realization(D0, rng)
+
+
+def _powlaw_stars(rng, K, n, ftc, mag_lo=15., mag_hi=23.3, alpha=2.):
+    fmin = mag2flux(mag_hi) * ftc
+    fmax = mag2flux(mag_lo) * ftc
+    f = gen_pow_law_sample(alpha, fmin, fmax, K, rng)
+    x = rng.random_sample(K) * (n - 2.) + 1.
+    y = rng.random_sample(K) * (n - 2.) + 1.
+    return f, x, y
+
+
+def make(name, n_chains=None, seed_offset=0):
+    name = name.upper()
+    img_rng = np.random.RandomState(77)
+    rng = np.random.RandomState(1000 + seed_offset)
+    if name in ("C1", "C2", "C4"):
+        n = 32 if name == "C1" else 48
+        par, ftc = base_params(dt=0.1)
+        f = mag2flux(19.) * ftc
+        if name == "C1":
+            xt, yt = 16.2, 15.7
+        else:
+            xt, yt = 24. + img_rng.uniform(-.5, .5), 24. + img_rng.uniform(-.5, .5)
+        D = _image(n, [(19., xt, yt)], ftc, par["B_count"], par["fwhm_pix"], img_rng)
+        nc = {"C1": 1, "C2": 4096, "C4": 1 << 20}[name] if n_chains is None else n_chains
+        if name == "C1":
+            q0 = np.array([[f, xt + 0.3, yt]]).repeat(nc, 0)
+        else:
+            q0 = np.stack([f * (1 + 0.1 * rng.randn(nc)), xt + 0.5 * rng.randn(nc),
+                           yt + 0.5 * rng.randn(nc)], 1)
+        K = 1
+        steps = 100 if name == "C1" else 500
+    elif name == "C3" or name == "C5":
+        n, K = (48, 10) if name == "C3" else (256, 64)
+        par, ftc = base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.,
+                               use_prior=(name == "C5"), alpha=2.)
+        ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc)
+        D = _image(n, [(22.5 - 2.5 * np.log10(a / ftc), b, c) for a, b, c in zip(ft, xt, yt)],
+                   ftc, par["B_count"], par["fwhm_pix"], img_rng)
+        nc = (16384 if name == "C3" else 8192) if n_chains is None else n_chains
+        # chains start at the truth, perturbed (flux x lognormal 10%, 0.5 px)
+        q0 = np.empty((nc, 3 * K))
+        q0[:, 0::3] = ft * np.exp(0.1 * rng.randn(nc, K))
+        q0[:, 1::3] = xt + 0.5 * rng.randn(nc, K)
+        q0[:, 2::3] = yt + 0.5 * rng.randn(nc, K)
+        steps = 500
+    else:
+        raise ValueError("unknown workload " + name)
+    H = metric_diag(q0, par)
+    p0 = rng.randn(*q0.shape) * np.sqrt(H)
+    note = "%s: %dx%d image, K=%d, %d chains, %d steps" % (name, n, n, K, nc, steps)
+    return Workload(name, D, q0, p0, par, steps, K, note)

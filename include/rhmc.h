@@ -1,0 +1,141 @@
+/*
+ * rhmc.h — C-ABI of the MI355X-native RHMC leapfrog engine (librhmc.so).
+ *
+ * Drop-in boundary for ONE hot path of jaekor91/HMC-stellar-toy-model: the
+ * implicit generalized-leapfrog step of the Riemannian-HMC sampler for the
+ * Poisson / Gaussian-PSF stellar-photometry posterior.
+ *
+ * Reference interface each entry point replaces (file:line into the
+ * reference checkout):
+ *   rhmc_leapfrog / rhmc_leapfrog_device
+ *       base_class.RHMC_single_step(q, p, delta, counter_max)
+ *       sampler_RHMC.py:522-566, called Nsteps times per MH iteration from
+ *       multi_gym.run_RHMC (sampler_RHMC.py:1053-1054) and inlined in
+ *       single_gym.run_single_RHMC solver="implicit" (:729-772).
+ *       n_steps consecutive steps are fused into one launch.
+ *   rhmc_gradient
+ *       base_class.dVdq (sampler_RHMC.py:365-425) and base_class.dphidq
+ *       (:448-465), batched over chains.
+ *   rhmc_energy
+ *       base_class.V (sampler_RHMC.py:294-351) and base_class.T (:353-363)
+ *       at H(q) (:229-258) — the trajectory-endpoint energies of the MH test
+ *       (:1021-1026, :1070-1071).
+ *   rhmc_ctx_create / rhmc_ctx_set_image
+ *       the instance attribute base_class.D set by gen_mock_data
+ *       (sampler_RHMC.py:77-99); uploaded once per context.
+ *   rhmc_params
+ *       the instance attributes the step reads: dt, g_xx,
+ *       g_ff, g_ff2, g0, g1, g2, B_count, f_lim, mB (-> f_low),
+ *       PSF_FWHM_pix, use_prior, alpha, use_Vc, beta, Vc_r_pow, plus the
+ *       run_RHMC arguments delta / counter_max (:937-939).
+ *
+ * Conventions
+ *   - Arrays are C-contiguous fp64 [n_chains][3K] with (f_k, x_k, y_k)
+ *     interleaved per star, flux in counts (format_q, sampler_RHMC.py:209).
+ *     D is fp64 [rows][cols], rows == cols (reference limitation:
+ *     gauss_PSF returns (cols, rows), utils.py:481-483).
+ *   - Host-pointer entry points are synchronous and update q, p in place.
+ *     The *_device entry points take device pointers and a hipStream_t
+ *     (passed as void*, NULL = the context's stream) and are asynchronous.
+ *   - Every call returns 0 on success or a negative RHMC_ERR_* code;
+ *     rhmc_last_error() gives a thread-local message.  No C++ exception
+ *     crosses the ABI.  A context must not be used by two threads at once;
+ *     one context per GPU.
+ */
+#ifndef RHMC_H
+#define RHMC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RHMC_ABI_VERSION 1
+
+enum {
+  RHMC_OK = 0,
+  RHMC_ERR_ARG = -1,         /* bad argument (shape, NULL, K range ...) */
+  RHMC_ERR_HIP = -2,         /* a HIP runtime call failed                */
+  RHMC_ERR_NOMEM = -3,       /* device allocation failed                 */
+  RHMC_ERR_UNSUPPORTED = -4  /* configuration not built into this library */
+};
+
+/* Per-chain status bits written by rhmc_leapfrog (OR over all steps). */
+#define RHMC_STATUS_NONFINITE   1u  /* q or p became NaN/inf                    */
+#define RHMC_STATUS_PLOOP_CAP   2u  /* p fixed-point loop stopped at counter_max */
+#define RHMC_STATUS_QLOOP_CAP   4u  /* q fixed-point loop stopped at counter_max */
+#define RHMC_STATUS_REFLECT_F   8u  /* flux-wall reflection (:558-559)           */
+#define RHMC_STATUS_REFLECT_XY 16u  /* edge reflection (:561-564)                */
+
+/* Instance state read by the step (POD; all fp64 except the flags). */
+typedef struct rhmc_params {
+  double dt;           /* self.dt                                            */
+  double delta;        /* fixed-point tolerance (absolute, max-norm)         */
+  double B_count;      /* background counts per pixel                        */
+  double f_lim;        /* flux wall (counts)                                 */
+  double f_low;        /* H_xx clamp = mag2flux(mB+2)*flux_to_count (:267)   */
+  double fwhm_pix;     /* PSF FWHM in pixels                                 */
+  double g_xx, g_ff, g_ff2;
+  double g0, g1, g2;   /* metric factors (utils.factors at 48x48, :165)      */
+  double alpha;        /* prior exponent (used when use_prior)               */
+  double beta;         /* repulsion strength (used when use_Vc)              */
+  double Vc_r_pow;     /* repulsion power                                    */
+  double V_prior_const;/* rhmc_energy only: the cached prior constant (:321) */
+  int32_t counter_max; /* fixed-point iteration cap                          */
+  int32_t use_prior;
+  int32_t use_Vc;
+  int32_t reserved;    /* must be 0                                          */
+} rhmc_params;
+
+typedef struct rhmc_ctx rhmc_ctx;
+
+/* ABI version of the loaded library (== RHMC_ABI_VERSION when in sync). */
+int rhmc_abi_version(void);
+/* Number of visible GPUs; 0 (and RHMC_OK) when none. */
+int rhmc_device_count(int* n);
+/* Thread-local message of the last failing call ("" if none). */
+const char* rhmc_last_error(void);
+
+/* Create a context on `device` and upload D [rows][cols] (host pointer). */
+int rhmc_ctx_create(int device, const double* D, int32_t rows, int32_t cols,
+                    rhmc_ctx** out);
+/* Replace the data image (host pointer); may change the size. */
+int rhmc_ctx_set_image(rhmc_ctx* ctx, const double* D, int32_t rows, int32_t cols);
+/* Device pointer of the context's image (for callers that keep state on device). */
+int rhmc_ctx_image_device(rhmc_ctx* ctx, const double** d_image);
+void rhmc_ctx_destroy(rhmc_ctx* ctx);
+/* Wait for all work queued on the context's stream. */
+int rhmc_ctx_synchronize(rhmc_ctx* ctx);
+
+/*
+ * n_steps RHMC_single_step()s on every chain.  q, p: host [n_chains][3K],
+ * updated in place.  fp_iters (nullable): host int32 [n_chains][2], the
+ * p- and q-loop iteration counts summed over the n_steps steps.  status
+ * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 64.
+ */
+int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p,
+                  int64_t n_chains, int32_t K, int32_t n_steps,
+                  int32_t* fp_iters, int32_t* status);
+
+/* Same on device-resident buffers, asynchronous on `stream` (hipStream_t). */
+int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
+                         double* d_p, int64_t n_chains, int32_t K,
+                         int32_t n_steps, int32_t* d_fp_iters,
+                         int32_t* d_status, void* stream);
+
+/* kind: 0 = dVdq (:365-425), 1 = dphidq (:448-465).  Host pointers. */
+int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
+                  double* grad, int64_t n_chains, int32_t K, int32_t kind);
+
+/* V (:294-351, with f_pos) and T at H(q) (:353-363) per chain.  V or T may
+ * be NULL.  p may be NULL when T is NULL.  Host pointers. */
+int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
+                const double* p, double* V, double* T, int64_t n_chains,
+                int32_t K, int32_t f_pos);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RHMC_H */

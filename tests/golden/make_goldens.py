@@ -1,0 +1,409 @@
+#!/usr/bin/env python3
+"""Generate golden fixtures from the REFERENCE implementation (build container only).
+
+This script is test infrastructure.  It never runs on the GPU box and it never
+vendors reference source: at run time it converts the reference's Python-2
+modules (`sampler_RHMC.py`, `utils.py`, `samplers.py` under /root/reference)
+with the standard-library `lib2to3` into a temporary directory OUTSIDE the
+repository, applies the two NumPy-2 shims the reference needs (`np.infty`,
+`np.product`, see SURVEY.md §4 bit-rot items 3), imports it, runs the cases
+below and writes small `.npz` fixtures next to this file.  Only inputs and
+outputs (data) are committed.
+
+Fixed-point iteration counts are not returned by the reference; they are
+recovered by counting calls to the instance's `dtaudq` / `dtaudp` inside one
+`RHMC_single_step` (sampler_RHMC.py:522-566): the p-loop calls `dtaudq` once
+per iteration and once more after the q-loop (:532, :548); the q-loop calls
+`dtaudp` twice per iteration (:542).
+
+Usage:  python tests/golden/make_goldens.py [--ref /root/reference]
+"""
+import argparse
+import contextlib
+import io
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def load_reference(ref_dir):
+    tmp = tempfile.mkdtemp(prefix="rhmc_ref_py3_")
+    for name in ("sampler_RHMC.py", "utils.py", "samplers.py"):
+        shutil.copy(os.path.join(ref_dir, name), tmp)
+    subprocess.run([sys.executable, "-m", "lib2to3", "-n", "-w",
+                    "sampler_RHMC.py", "utils.py", "samplers.py"],
+                   cwd=tmp, check=True, stdout=subprocess.DEVNULL,
+                   stderr=subprocess.DEVNULL)
+    np.infty = np.inf          # removed in NumPy 2 (sampler_RHMC.py:312,317,529)
+    np.product = np.prod       # removed in NumPy 2 (samplers.py:911)
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    sys.path.insert(0, tmp)
+    import sampler_RHMC  # noqa: E402
+    import utils         # noqa: E402
+    return sampler_RHMC, utils, tmp
+
+
+class Counter:
+    """Wrap a gym's dtaudq/dtaudp to count calls (fixed-point iterations)."""
+
+    def __init__(self, gym):
+        self.gym = gym
+        self.n_tq = 0
+        self.n_tp = 0
+        orig_q, orig_p = gym.dtaudq, gym.dtaudp
+
+        def dtaudq(q, p):
+            self.n_tq += 1
+            return orig_q(q, p)
+
+        def dtaudp(q, p):
+            self.n_tp += 1
+            return orig_p(q, p)
+
+        gym.dtaudq = dtaudq
+        gym.dtaudp = dtaudp
+
+    def step(self, q, p, delta, cmax):
+        self.n_tq = self.n_tp = 0
+        q1, p1 = self.gym.RHMC_single_step(q, p, delta=delta, counter_max=cmax)
+        return q1, p1, self.n_tq - 1, self.n_tp // 2
+
+
+def gym_params(g):
+    """Every instance attribute the hot path reads."""
+    f_low = g.mag2flux_converter(g.mB + 2)
+    return dict(
+        rows=g.num_rows, cols=g.num_cols, dt=g.dt, B_count=g.B_count,
+        f_lim=g.f_lim, f_low=f_low, fwhm_pix=g.PSF_FWHM_pix, g_xx=g.g_xx,
+        g_ff=g.g_ff, g_ff2=g.g_ff2, g0=g.g0, g1=g.g1, g2=g.g2,
+        use_prior=int(bool(g.use_prior)), alpha=g.alpha,
+        use_Vc=int(bool(g.use_Vc)), beta=g.beta, Vc_r_pow=g.Vc_r_pow,
+        fmin=-1.0 if getattr(g, "fmin", None) is None else g.fmin,
+        fmax=-1.0 if getattr(g, "fmax", None) is None else g.fmax,
+        flux_to_count=g.flux_to_count, mB=g.mB)
+
+
+def pack(prefix, d):
+    return {prefix + k: np.asarray(v) for k, v in d.items()}
+
+
+def make_gym(S, cls="multi", n=48, g_xx=1., g_ff=1., g_ff2=1., dt=0.1,
+             prior=False, alpha=2., fminmax=(20., 15.)):
+    g = (S.multi_gym if cls == "multi" else S.single_gym)(
+        dt=0., Nsteps=0, g_xx=g_xx, g_ff=g_ff, g_ff2=g_ff2)
+    g.num_rows = g.num_cols = n          # factors g0..g2 stay at 48x48 (quirk)
+    g.dt = dt
+    g.fmin = g.mag2flux_converter(fminmax[0])
+    g.fmax = g.mag2flux_converter(fminmax[1])
+    if prior:
+        g.use_prior = True
+        g.alpha = alpha
+    return g
+
+
+def stars_to_q(g, stars):
+    """(K,3) mag,x,y -> flat f,x,y in counts (format_q, sampler_RHMC.py:209)."""
+    q = np.array(stars, dtype=float).copy()
+    return g.format_q(q)
+
+
+def trajectory(g, q, p, nsteps, delta=1e-6, cmax=1000):
+    c = Counter(g)
+    Q = [q.copy()]
+    P = [p.copy()]
+    NP, NQ = [], []
+    for _ in range(nsteps):
+        q, p, a, b = c.step(q, p, delta, cmax)
+        Q.append(q.copy())
+        P.append(p.copy())
+        NP.append(a)
+        NQ.append(b)
+    return np.array(Q), np.array(P), np.array(NP, np.int32), np.array(NQ, np.int32)
+
+
+# ----------------------------------------------------------------------------
+# Case 1: per-function vectors (gauss_PSF, dVdq, H, dphidq, dtaudq, dtaudp, V, T)
+# ----------------------------------------------------------------------------
+def case_functions(S, U):
+    out = {}
+    rs = np.random.RandomState(5)
+    # gauss_PSF (utils.py:475-486): square and rectangular (shape quirk)
+    psf_args = [(48, 48, 24.3, 23.8), (32, 32, 0.2, 31.7), (16, 16, 8.0, 8.0),
+                (4, 6, 1.3, 2.2)]
+    for i, (r, c, x, y) in enumerate(psf_args):
+        out["psf%d_args" % i] = np.array([r, c, x, y, 1.4 / 0.4])
+        out["psf%d" % i] = U.gauss_PSF(r, c, x, y, FWHM=1.4 / 0.4)
+
+    # factors (utils.py:623-644) at a few grids
+    out["factors_args"] = np.array([[48, 48, 24., 24.], [32, 32, 16., 16.],
+                                    [64, 64, 32.3, 31.6]])
+    out["factors"] = np.array([U.factors(int(a), int(b), x, y, 1.4 / 0.4)
+                               for a, b, x, y in out["factors_args"]])
+
+    sets = [
+        # name, n, stars(true), gym kwargs, K_model
+        ("k1", 48, [[19., 24.3, 23.8]], dict(), 1),
+        ("k1gff2", 48, [[20., 24.3, 23.8]], dict(g_ff2=2.), 1),
+        ("k10", 48, None, dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05,
+                                prior=True), 10),
+        ("vc5", 32, None, dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05), 5),
+    ]
+    for name, n, stars, kw, K in sets:
+        np.random.seed(77)
+        g = make_gym(S, n=n, **kw)
+        if stars is None:
+            fmin = g.mag2flux_converter(23.)
+            fmax = g.mag2flux_converter(15.)
+            mags = g.flux2mag_converter(U.gen_pow_law_sample(2., fmin, fmax, K))
+            xs = np.random.random(K) * (n - 2.) + 1.
+            ys = np.random.random(K) * (n - 2.) + 1.
+            stars = np.stack([mags, xs, ys], 1)
+        if name == "vc5":
+            g.use_Vc = True
+            g.beta = 1e-2
+            g.f_expnt = np.zeros(K)
+            g.Vc_r_pow = 2.
+        g.gen_mock_data(np.array(stars))
+        g.Nobjs = K
+        g.d = 3 * K
+        q_true = stars_to_q(g, stars)
+        qs, ps = [], []
+        for t in range(6):
+            q = q_true.copy()
+            q[0::3] *= np.exp(0.2 * rs.randn(K))
+            q[1::3] += 0.7 * rs.randn(K)
+            q[2::3] += 0.7 * rs.randn(K)
+            if t == 5:      # one flux below f_low (H_xx clamp branch, :269-276)
+                q[0] = 0.5 * g.mag2flux_converter(g.mB + 2)
+            qs.append(q)
+            ps.append(rs.randn(3 * K) * np.sqrt(np.abs(g.H(q))))
+        qs, ps = np.array(qs), np.array(ps)
+        res = dict(D=g.D, q=qs, p=ps)
+        res["dVdq"] = np.array([g.dVdq(q) for q in qs])
+        res["H"] = np.array([g.H(q) for q in qs])
+        hg = [g.H(q, grad=True) for q in qs]
+        res["Hv"] = np.array([h[0] for h in hg])
+        res["Hg"] = np.array([h[1] for h in hg])
+        res["dphidq"] = np.array([g.dphidq(q) for q in qs])
+        res["dtaudq"] = np.array([g.dtaudq(q, p) for q, p in zip(qs, ps)])
+        res["dtaudp"] = np.array([g.dtaudp(q, p) for q, p in zip(qs, ps)])
+        res["V"] = np.array([g.V(q, f_pos=False) for q in qs])
+        res["Vpos"] = np.array([g.V(q, f_pos=True) for q in qs])
+        res["T"] = np.array([g.T(p, g.H(q)) for q, p in zip(qs, ps)])
+        params = gym_params(g)
+        if g.use_Vc:
+            params["f_expnt_present"] = 1
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", params))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Case 2: single steps incl. flux-wall and edge reflections
+# ----------------------------------------------------------------------------
+def case_steps(S, U):
+    np.random.seed(77)
+    g = make_gym(S, n=48)
+    g.gen_mock_data(np.array([[19., 24.3, 23.8]]))
+    g.Nobjs, g.d = 1, 3
+    c = Counter(g)
+    rs = np.random.RandomState(11)
+    f19 = g.mag2flux_converter(19.)
+    Q0, P0, Q1, P1, NP, NQ = [], [], [], [], [], []
+    for t in range(48):
+        q = np.array([f19 * np.exp(0.3 * rs.randn()), 24.3 + rs.randn(),
+                      23.8 + rs.randn()])
+        if t % 8 == 1:      # flux just above the wall, moving down
+            q[0] = g.f_lim * (1 + 1e-3 * rs.rand())
+        if t % 8 == 2:      # near the x edge
+            q[1] = 0.02 * rs.rand()
+        if t % 8 == 3:      # near the far y edge
+            q[2] = g.num_cols - 1 - 0.02 * rs.rand()
+        if t % 8 == 4:      # flux under f_low: H_xx clamp (:269)
+            q[0] = 3.0
+        p = rs.randn(3) * np.sqrt(g.H(q))
+        if t % 8 == 1:
+            p[0] = -abs(p[0]) * 50
+        if t % 8 == 2:
+            p[1] = -abs(p[1]) * 5
+        if t % 8 == 3:
+            p[2] = abs(p[2]) * 5
+        q1, p1, a, b = c.step(q, p, 1e-6, 1000)
+        Q0.append(q); P0.append(p); Q1.append(q1); P1.append(p1)
+        NP.append(a); NQ.append(b)
+    res = dict(D=g.D, q0=np.array(Q0), p0=np.array(P0), q1=np.array(Q1),
+               p1=np.array(P1), n_p=np.array(NP, np.int32),
+               n_q=np.array(NQ, np.int32))
+    out = pack("", res)
+    out.update(pack("par_", gym_params(g)))
+    return out
+
+
+# ----------------------------------------------------------------------------
+# Case 3: trajectories (configs C1, C2-geometry, C3-geometry, C5-geometry, ...)
+# ----------------------------------------------------------------------------
+def traj_case(S, U, n, stars_true, model_fn, kw, nchains, nsteps, seed=77,
+              vc=None, cmax=1000, delta=1e-6, p_mod=None):
+    np.random.seed(seed)
+    g = make_gym(S, n=n, **kw)
+    if callable(stars_true):
+        stars_true = stars_true(g)
+    if vc is not None:
+        g.use_Vc = True
+        g.beta, g.Vc_r_pow = vc
+    g.gen_mock_data(np.array(stars_true, dtype=float))
+    Qs, Ps, NPs, NQs = [], [], [], []
+    for c in range(nchains):
+        stars = model_fn(g, c)
+        K = len(stars)
+        g.Nobjs, g.d = K, 3 * K
+        if vc is not None:
+            g.f_expnt = np.zeros(K)
+        q0 = stars_to_q(g, stars)
+        p0 = np.random.randn(3 * K) * np.sqrt(g.H(q0))
+        if p_mod is not None:
+            p0 = p_mod(g, c, p0)
+        Q, P, NP, NQ = trajectory(g, q0, p0, nsteps, delta, cmax)
+        Qs.append(Q); Ps.append(P); NPs.append(NP); NQs.append(NQ)
+    res = dict(D=g.D, Q=np.array(Qs), P=np.array(Ps), n_p=np.array(NPs),
+               n_q=np.array(NQs), delta=delta, counter_max=cmax)
+    out = pack("", res)
+    out.update(pack("par_", gym_params(g)))
+    return out
+
+
+def powlaw_stars(U, g, K, n, mag_lo=15., mag_hi=23.3, alpha=2.):
+    fmin = g.mag2flux_converter(mag_hi)
+    fmax = g.mag2flux_converter(mag_lo)
+    mags = g.flux2mag_converter(U.gen_pow_law_sample(alpha, fmin, fmax, K))
+    xs = np.random.random(K) * (n - 2.) + 1.
+    ys = np.random.random(K) * (n - 2.) + 1.
+    return np.stack([mags, xs, ys], 1)
+
+
+def case_trajs(S, U):
+    cases = {}
+    # C1: 32x32, K=1, mag 19 at (16.2, 15.7), init x+0.3, 100 steps, 1 chain
+    cases["traj_c1"] = traj_case(
+        S, U, 32, [[19., 16.2, 15.7]], lambda g, c: [[19., 16.5, 15.7]],
+        dict(), 1, 100)
+    # C2 geometry: 48x48 K=1 mag 19, 8 chains x 500 steps
+    rs = np.random.RandomState(1000)
+    jit = rs.randn(8, 3)
+    cases["traj_c2"] = traj_case(
+        S, U, 48, [[19., 24.21, 23.86]],
+        lambda g, c: [[19. - 2.5 * np.log10(1 + 0.1 * jit[c, 0]),
+                       24.21 + 0.5 * jit[c, 1], 23.86 + 0.5 * jit[c, 2]]],
+        dict(), 8, 500)
+    # g_ff2 != 1 (H_ff grad quirk, :292), base_class default g_ff2=2
+    cases["traj_gff2"] = traj_case(
+        S, U, 48, [[20., 24.21, 23.86]],
+        lambda g, c: [[20.2, 24.0 + 0.3 * c, 23.9]], dict(g_ff2=2.), 2, 200)
+    # C3 geometry: 48x48 K=10 big-sim4 parameters + flux wall reflections
+    cases["traj_c3"] = traj_case(
+        S, U, 48, lambda g: powlaw_stars(U, g, 10, 48),
+        lambda g, c: powlaw_stars(U, g, 10, 48),
+        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05), 2, 300)
+    # prior on (use_prior, :408-409)
+    cases["traj_prior"] = traj_case(
+        S, U, 32, lambda g: powlaw_stars(U, g, 3, 32),
+        lambda g, c: powlaw_stars(U, g, 3, 32),
+        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True), 2, 200)
+    # repulsion on (use_Vc, :411-418)
+    cases["traj_vc"] = traj_case(
+        S, U, 32, lambda g: powlaw_stars(U, g, 5, 32),
+        lambda g, c: powlaw_stars(U, g, 5, 32),
+        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05), 2, 100, vc=(1e-2, 2.))
+    # edge: star drifting through the x=0 boundary
+    cases["traj_edge"] = traj_case(
+        S, U, 32, [[17., 0.6, 16.]], lambda g, c: [[17.2, 0.3 + 0.2 * c, 16.1]],
+        dict(dt=0.2), 2, 200,
+        p_mod=lambda g, c, p: p * np.array([1., 0., 1.]) + np.array(
+            [0., -(40. + 20. * c), 0.]) * np.sqrt(g.H(p * 0 + np.array(
+                [g.mag2flux_converter(17.2), 0., 0.]))))
+    # small counter_max (loop cut off) and looser delta
+    cases["traj_cmax"] = traj_case(
+        S, U, 48, [[16., 24.2, 23.9]], lambda g, c: [[16.5, 24.6, 23.3]],
+        dict(dt=0.3), 2, 100, cmax=2, delta=1e-9)
+    # C5 geometry: 256x256 K=64, prior, big-sim4 parameters, 3 steps, 1 chain
+    cases["traj_c5"] = traj_case(
+        S, U, 256, lambda g: powlaw_stars(U, g, 64, 256),
+        lambda g, c: powlaw_stars(U, g, 64, 256),
+        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True), 1, 3)
+    return cases
+
+
+# ----------------------------------------------------------------------------
+# Case 4: full MH loop (multi_gym.run_RHMC move-0 branch) and single_gym trace
+# ----------------------------------------------------------------------------
+def case_mh(S, U):
+    out = {}
+    for name, n, stars_t, stars_m, kw, niter, nsteps, dt in [
+        ("mh1", 32, [[19., 16.2, 15.7]], [[19.5, 16.6, 15.2]], dict(), 30, 10,
+         0.1),
+        ("mh3", 32, [[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4], [19.6, 15.3, 24.6]],
+         dict(g_xx=0.05, g_ff=4., g_ff2=4., prior=True), 20, 10, 0.05),
+    ]:
+        np.random.seed(77)
+        g = make_gym(S, n=n, **kw)
+        g.gen_mock_data(np.array(stars_t))
+        np.random.seed(123)
+        with contextlib.redirect_stdout(io.StringIO()):
+            g.run_RHMC(np.array(stars_m), f_pos=True, delta=1e-6, Niter=niter,
+                       Nsteps=nsteps, dt=dt, N_max=len(stars_m))
+        res = dict(D=g.D, q_model=np.array(stars_m), q_chain=g.q_chain,
+                   p_chain=g.p_chain, E_chain=g.E_chain, V_chain=g.V_chain,
+                   T_chain=g.T_chain, A_chain=g.A_chain.astype(np.int32),
+                   niter=niter, nsteps=nsteps, seed=123, dt=dt)
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+
+    # single_gym.run_single_RHMC(solver="implicit") energy trace (:649-783)
+    np.random.seed(77)
+    g = S.single_gym(dt=0., Nsteps=0, g_xx=1., g_ff=1.)
+    g.num_rows = g.num_cols = 16
+    g.fmin = g.mag2flux_converter(20.)   # V needs fmin/fmax (:320-321)
+    g.fmax = g.mag2flux_converter(15.)
+    g.gen_mock_data(np.array([[19., 8., 8.]]))
+    g.Nsteps, g.dt = 100, 0.1
+    np.random.seed(5)
+    g.run_single_RHMC(q_model_0=np.array([[19., 9., 8.]]), f_pos=True,
+                      solver="implicit", delta=1e-6)
+    res = dict(D=g.D, q_chain=g.q_chain, p_chain=g.p_chain, E_chain=g.E_chain,
+               V_chain=g.V_chain, T_chain=g.T_chain)
+    out.update(pack("single/", res))
+    out.update(pack("single/par_", gym_params(g)))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    S, U, tmp = load_reference(args.ref)
+    try:
+        jobs = {"functions": case_functions, "steps": case_steps,
+                "mh": case_mh}
+        for name, fn in jobs.items():
+            if args.only and args.only != name:
+                continue
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), **fn(S, U))
+            print("wrote", name)
+        if not args.only or args.only == "trajs":
+            for name, d in case_trajs(S, U).items():
+                np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+                print("wrote", name)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+"""GPU parity: the HIP path (through the C-ABI) against the reference goldens
+and the CPU oracle.
+
+Tolerances (fp64): gradients and energies to 1e-10 relative to the value
+scale; one step to 1e-11; trajectories to 1e-9 (q) / 1e-8 (p) relative to
+|value|+1 after up to 500 steps (SURVEY §8(c) measured that 1e-15 input
+perturbations grow to <= 8e-12 / 1.3e-10 over 500 steps).  Fixed-point
+iteration counts must match the reference exactly on every step.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from helpers import assert_state_close, capi_params
+from oracle import rhmc_ref as R
+
+pytestmark = pytest.mark.gpu
+
+
+def _ctx(capi, z):
+    return capi.Context(z["D"])
+
+
+@pytest.mark.parametrize("name", ["k1", "k1gff2", "k10", "vc5"])
+def test_gradient_and_energy(gpu_lib, name):
+    capi = gpu_lib
+    z = load_golden("functions")
+    par = R.params_from_npz(z, name + "/par_")
+    ctx = capi.Context(z[name + "/D"])
+    P = capi_params(capi, par)
+    q, p = z[name + "/q"], z[name + "/p"]
+    for kind, key in ((0, "dVdq"), (1, "dphidq")):
+        g = ctx.gradient(P, q, kind=kind)
+        want = z[name + "/" + key]
+        scale = np.abs(want).max(axis=1, keepdims=True) + 1.0
+        np.testing.assert_array_less(np.abs(g - want) / scale, 1e-10)
+    V, T = ctx.energy(P, q, p, f_pos=False)
+    np.testing.assert_allclose(V, z[name + "/V"], rtol=1e-12)
+    np.testing.assert_allclose(T, z[name + "/T"], rtol=1e-12, atol=1e-12)
+    Vp, _ = ctx.energy(P, q, None, f_pos=True)
+    want = z[name + "/Vpos"]
+    assert np.array_equal(np.isinf(Vp), np.isinf(want))
+    fin = np.isfinite(want)
+    np.testing.assert_allclose(Vp[fin], want[fin], rtol=1e-12)
+
+
+def test_single_steps(gpu_lib):
+    capi = gpu_lib
+    z = load_golden("steps")
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par)
+    q1, p1, it, st = ctx.leapfrog(P, z["q0"], z["p0"], 1, return_info=True)
+    np.testing.assert_array_equal(it[:, 0], z["n_p"])
+    np.testing.assert_array_equal(it[:, 1], z["n_q"])
+    assert_state_close(q1, z["q1"], 1e-11, "q")
+    assert_state_close(p1, z["p1"], 1e-10, "p")
+    # the status word reports the reflections that fired
+    m = R.RefModel(z["D"], par)
+    for c in range(len(q1)):
+        refl_f = z["q1"][c, 0] < par["f_lim"]
+        assert bool(st[c] & capi.STATUS_REFLECT_F) == refl_f
+
+
+TRAJ = [("traj_c1", 1e-9, 1e-8), ("traj_c2", 1e-9, 1e-8), ("traj_gff2", 1e-9, 1e-8),
+        ("traj_c3", 1e-9, 1e-8), ("traj_prior", 1e-9, 1e-8), ("traj_vc", 1e-9, 1e-8),
+        ("traj_edge", 1e-9, 1e-8), ("traj_cmax", 1e-9, 1e-8)]
+
+
+@pytest.mark.parametrize("name,qtol,ptol", TRAJ)
+def test_trajectory_stepwise(gpu_lib, name, qtol, ptol):
+    """One launch per step: every intermediate state and iteration count."""
+    capi = gpu_lib
+    z = load_golden(name)
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par, float(z["delta"]), int(z["counter_max"]))
+    Q, Pm = z["Q"], z["P"]
+    q, p = Q[:, 0].copy(), Pm[:, 0].copy()
+    nsteps = Q.shape[1] - 1
+    for s in range(nsteps):
+        q, p, it, _ = ctx.leapfrog(P, q, p, 1, return_info=True)
+        np.testing.assert_array_equal(it[:, 0], z["n_p"][:, s], err_msg="p-iters step %d" % s)
+        np.testing.assert_array_equal(it[:, 1], z["n_q"][:, s], err_msg="q-iters step %d" % s)
+        assert_state_close(q, Q[:, s + 1], qtol, "%s q step %d" % (name, s))
+        assert_state_close(p, Pm[:, s + 1], ptol, "%s p step %d" % (name, s))
+
+
+@pytest.mark.parametrize("name,qtol,ptol", TRAJ)
+def test_trajectory_fused(gpu_lib, name, qtol, ptol):
+    """All steps fused in one launch (the production path)."""
+    capi = gpu_lib
+    z = load_golden(name)
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par, float(z["delta"]), int(z["counter_max"]))
+    Q, Pm = z["Q"], z["P"]
+    nsteps = Q.shape[1] - 1
+    q, p, it, st = ctx.leapfrog(P, Q[:, 0], Pm[:, 0], nsteps, return_info=True)
+    np.testing.assert_array_equal(it[:, 0], z["n_p"].sum(1))
+    np.testing.assert_array_equal(it[:, 1], z["n_q"].sum(1))
+    assert_state_close(q, Q[:, -1], qtol, name + " q")
+    assert_state_close(p, Pm[:, -1], ptol, name + " p")
+    assert not (st & capi.STATUS_NONFINITE).any()
+
+
+def test_chains_independent(gpu_lib):
+    """A batch gives exactly the per-chain results (no cross-chain coupling)."""
+    capi = gpu_lib
+    z = load_golden("traj_c2")
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par)
+    rs = np.random.RandomState(3)
+    n = 37
+    q0 = np.repeat(z["Q"][:, 0], 5, axis=0)[:n] * (1 + 1e-3 * rs.randn(n, 3))
+    p0 = np.repeat(z["P"][:, 0], 5, axis=0)[:n]
+    qb, pb = ctx.leapfrog(P, q0, p0, 20)
+    for c in (0, 5, 17, 36):
+        qs, ps = ctx.leapfrog(P, q0[c], p0[c], 20)
+        assert np.array_equal(qs, qb[c]) and np.array_equal(ps, pb[c])
+
+
+def test_oracle_matches_gpu_random_chains(gpu_lib):
+    """Seeded random chains at C2 geometry: GPU vs the CPU oracle, 100 steps."""
+    capi = gpu_lib
+    z = load_golden("traj_c2")
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par)
+    m = R.RefModel(z["D"], par)
+    rs = np.random.RandomState(21)
+    n = 6
+    q0 = np.tile(z["Q"][0, 0], (n, 1)) * np.array([1, 0, 0]) + np.c_[
+        z["Q"][0, 0, 0] * np.exp(0.2 * rs.randn(n)), 24 + rs.randn(n), 24 + rs.randn(n)]
+    p0 = rs.randn(n, 3) * np.sqrt(np.array([m.H(q) for q in q0]))
+    qg, pg, it, _ = ctx.leapfrog(P, q0, p0, 100, return_info=True)
+    for c in range(n):
+        qo, po, NP, NQ = m.trajectory(q0[c], p0[c], 100, record=False)
+        assert it[c, 0] == NP.sum() and it[c, 1] == NQ.sum()
+        assert_state_close(qg[c], qo, 1e-9, "q")
+        assert_state_close(pg[c], po, 1e-8, "p")
+
+
+def test_errors(gpu_lib):
+    capi = gpu_lib
+    z = load_golden("traj_c1")
+    par = R.params_from_npz(z)
+    with pytest.raises(capi.RhmcError):
+        capi.Context(np.zeros((4, 6)))          # rows != cols
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par)
+    with pytest.raises(capi.RhmcError):
+        ctx.leapfrog(P, np.zeros((2, 3 * 65)), np.zeros((2, 3 * 65)), 1)   # K > 64
+    bad = capi_params(capi, par)
+    bad.reserved = 1
+    with pytest.raises(capi.RhmcError):
+        ctx.leapfrog(bad, z["Q"][:, 0], z["P"][:, 0], 1)
+    # zero chains and zero steps are no-ops
+    q, p = ctx.leapfrog(P, z["Q"][:, 0], z["P"][:, 0], 0)
+    assert np.array_equal(q, z["Q"][:, 0]) and np.array_equal(p, z["P"][:, 0])

@@ -1,0 +1,80 @@
+"""Pin the CPU oracle (oracle/rhmc_ref.py) to the reference's own outputs.
+
+The golden vectors were produced by running the reference itself
+(tests/golden/make_goldens.py).  The oracle restates the same NumPy
+expressions in the same order, so agreement is expected to the last ulp or
+so; trajectories must reproduce the per-step fixed-point iteration counts
+exactly.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import rhmc_ref as R
+
+
+def test_constants_match_reference():
+    z = load_golden("functions")
+    par = R.params_from_npz(z, "k1/par_")
+    d = R.default_setup()
+    for k in ("B_count", "f_lim", "f_low", "flux_to_count"):
+        assert d[k] == par[k], k
+    assert d["fwhm_pix"] == par["fwhm_pix"]
+    g = R.factors(48, 48, 24., 24., d["fwhm_pix"])
+    assert g == (par["g0"], par["g1"], par["g2"])     # bit-exact
+
+
+def test_gauss_psf_and_factors():
+    z = load_golden("functions")
+    for i in range(4):
+        r, c, x, y, fw = z["psf%d_args" % i]
+        np.testing.assert_array_equal(R.gauss_psf(int(r), int(c), x, y, fw), z["psf%d" % i])
+    for args, want in zip(z["factors_args"], z["factors"]):
+        got = R.factors(int(args[0]), int(args[1]), args[2], args[3], 1.4 / 0.4)
+        np.testing.assert_array_equal(np.array(got), want)
+
+
+@pytest.mark.parametrize("name", ["k1", "k1gff2", "k10", "vc5"])
+def test_functions(name):
+    z = load_golden("functions")
+    par = R.params_from_npz(z, name + "/par_")
+    m = R.RefModel(z[name + "/D"], par)
+    qs, ps = z[name + "/q"], z[name + "/p"]
+    tol = dict(rtol=1e-13, atol=1e-13)
+    for i, (q, p) in enumerate(zip(qs, ps)):
+        np.testing.assert_allclose(m.dVdq(q), z[name + "/dVdq"][i], **tol)
+        np.testing.assert_allclose(m.H(q), z[name + "/H"][i], rtol=1e-15)
+        hv, hg = m.H(q, grad=True)
+        np.testing.assert_allclose(hv, z[name + "/Hv"][i], rtol=1e-15)
+        np.testing.assert_allclose(hg, z[name + "/Hg"][i], rtol=1e-15)
+        np.testing.assert_allclose(m.dphidq(q), z[name + "/dphidq"][i], **tol)
+        np.testing.assert_allclose(m.dtaudq(q, p), z[name + "/dtaudq"][i], rtol=1e-15)
+        np.testing.assert_allclose(m.dtaudp(q, p), z[name + "/dtaudp"][i], rtol=1e-15)
+        np.testing.assert_allclose(m.V(q), z[name + "/V"][i], rtol=1e-14)
+        np.testing.assert_allclose(m.V(q, f_pos=True), z[name + "/Vpos"][i], rtol=1e-14)
+        np.testing.assert_allclose(m.T(p, m.H(q)), z[name + "/T"][i], rtol=1e-14)
+
+
+def test_single_steps_exact():
+    z = load_golden("steps")
+    m = R.RefModel(z["D"], R.params_from_npz(z))
+    for i in range(len(z["q0"])):
+        q1, p1, a, b = m.step(z["q0"][i], z["p0"][i])
+        assert (a, b) == (z["n_p"][i], z["n_q"][i])
+        np.testing.assert_allclose(q1, z["q1"][i], rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(p1, z["p1"][i], rtol=1e-11, atol=1e-11)
+
+
+@pytest.mark.parametrize("name,steps", [("traj_c1", 100), ("traj_c2", 60), ("traj_gff2", 200),
+                                        ("traj_c3", 40), ("traj_prior", 80), ("traj_vc", 50),
+                                        ("traj_edge", 200), ("traj_cmax", 100)])
+def test_trajectories(name, steps):
+    z = load_golden(name)
+    m = R.RefModel(z["D"], R.params_from_npz(z))
+    delta, cmax = float(z["delta"]), int(z["counter_max"])
+    for c in range(z["Q"].shape[0]):
+        Q, P, NP, NQ = m.trajectory(z["Q"][c, 0], z["P"][c, 0], steps, delta, cmax)
+        np.testing.assert_array_equal(NP, z["n_p"][c, :steps])
+        np.testing.assert_array_equal(NQ, z["n_q"][c, :steps])
+        np.testing.assert_allclose(Q, z["Q"][c, :steps + 1], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(P, z["P"][c, :steps + 1], rtol=1e-8, atol=1e-8)
