@@ -136,7 +136,9 @@ def main():
     p = torch.from_numpy(wl.p0).to(dev).contiguous()
     it = torch.zeros((wl.n_chains, 2), dtype=torch.int32, device=dev)
     st = torch.zeros(wl.n_chains, dtype=torch.int32, device=dev)
-    stream = torch.cuda.current_stream(dev)
+    # A dedicated (non-null) torch stream: the kernel is launched on it and the
+    # timing events are recorded on it.
+    stream = torch.cuda.Stream(dev)
 
     def launch():
         ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,

@@ -62,45 +62,53 @@ def test_single_steps(gpu_lib):
         assert bool(st[c] & capi.STATUS_REFLECT_F) == refl_f
 
 
-TRAJ = [("traj_c1", 1e-9, 1e-8), ("traj_c2", 1e-9, 1e-8), ("traj_gff2", 1e-9, 1e-8),
-        ("traj_c3", 1e-9, 1e-8), ("traj_prior", 1e-9, 1e-8), ("traj_vc", 1e-9, 1e-8),
-        ("traj_edge", 1e-9, 1e-8), ("traj_cmax", 1e-9, 1e-8)]
+# (golden, q tol, p tol, free-running horizon).  traj_c3 (K=10, big-sim4
+# parameters, stars wandering through the edges) is chaotic: the reference
+# itself, started 1e-15 away, leaves 1e-9 agreement after ~130 steps
+# (measured with the oracle), so its free-running comparison stops at 100
+# steps; every one of its 300 steps is still checked locally (reset to the
+# golden state each step).
+TRAJ = [("traj_c1", 1e-9, 1e-8, None), ("traj_c2", 1e-9, 1e-8, None),
+        ("traj_gff2", 1e-9, 1e-8, None), ("traj_c3", 1e-9, 1e-8, 100),
+        ("traj_prior", 1e-9, 1e-8, None), ("traj_vc", 1e-9, 1e-8, None),
+        ("traj_edge", 1e-9, 1e-8, None), ("traj_cmax", 1e-9, 1e-8, None)]
 
 
-@pytest.mark.parametrize("name,qtol,ptol", TRAJ)
-def test_trajectory_stepwise(gpu_lib, name, qtol, ptol):
-    """One launch per step: every intermediate state and iteration count."""
+@pytest.mark.parametrize("name,qtol,ptol,horizon", TRAJ)
+def test_trajectory_stepwise(gpu_lib, name, qtol, ptol, horizon):
+    """Every step of the reference trajectory, one launch per step, each
+    started from the reference's own state: local error <= 1e-11 and the
+    exact fixed-point iteration counts."""
     capi = gpu_lib
     z = load_golden(name)
     par = R.params_from_npz(z)
     ctx = _ctx(capi, z)
     P = capi_params(capi, par, float(z["delta"]), int(z["counter_max"]))
     Q, Pm = z["Q"], z["P"]
-    q, p = Q[:, 0].copy(), Pm[:, 0].copy()
     nsteps = Q.shape[1] - 1
     for s in range(nsteps):
-        q, p, it, _ = ctx.leapfrog(P, q, p, 1, return_info=True)
+        q, p, it, _ = ctx.leapfrog(P, Q[:, s], Pm[:, s], 1, return_info=True)
         np.testing.assert_array_equal(it[:, 0], z["n_p"][:, s], err_msg="p-iters step %d" % s)
         np.testing.assert_array_equal(it[:, 1], z["n_q"][:, s], err_msg="q-iters step %d" % s)
-        assert_state_close(q, Q[:, s + 1], qtol, "%s q step %d" % (name, s))
-        assert_state_close(p, Pm[:, s + 1], ptol, "%s p step %d" % (name, s))
+        assert_state_close(q, Q[:, s + 1], 1e-11, "%s q step %d" % (name, s))
+        assert_state_close(p, Pm[:, s + 1], 1e-10, "%s p step %d" % (name, s))
 
 
-@pytest.mark.parametrize("name,qtol,ptol", TRAJ)
-def test_trajectory_fused(gpu_lib, name, qtol, ptol):
-    """All steps fused in one launch (the production path)."""
+@pytest.mark.parametrize("name,qtol,ptol,horizon", TRAJ)
+def test_trajectory_fused(gpu_lib, name, qtol, ptol, horizon):
+    """Free-running: all steps fused in one launch (the production path)."""
     capi = gpu_lib
     z = load_golden(name)
     par = R.params_from_npz(z)
     ctx = _ctx(capi, z)
     P = capi_params(capi, par, float(z["delta"]), int(z["counter_max"]))
     Q, Pm = z["Q"], z["P"]
-    nsteps = Q.shape[1] - 1
+    nsteps = Q.shape[1] - 1 if horizon is None else horizon
     q, p, it, st = ctx.leapfrog(P, Q[:, 0], Pm[:, 0], nsteps, return_info=True)
-    np.testing.assert_array_equal(it[:, 0], z["n_p"].sum(1))
-    np.testing.assert_array_equal(it[:, 1], z["n_q"].sum(1))
-    assert_state_close(q, Q[:, -1], qtol, name + " q")
-    assert_state_close(p, Pm[:, -1], ptol, name + " p")
+    np.testing.assert_array_equal(it[:, 0], z["n_p"][:, :nsteps].sum(1))
+    np.testing.assert_array_equal(it[:, 1], z["n_q"][:, :nsteps].sum(1))
+    assert_state_close(q, Q[:, nsteps], qtol, name + " q")
+    assert_state_close(p, Pm[:, nsteps], ptol, name + " p")
     assert not (st & capi.STATUS_NONFINITE).any()
 
 
