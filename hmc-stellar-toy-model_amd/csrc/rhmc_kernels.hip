@@ -22,10 +22,12 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
 #include "rhmc.h"
+#include "rhmc_tiled.hpp"
 #include "rhmc_wave.hpp"
 
 namespace rhmc {
@@ -583,6 +585,27 @@ struct EnergyLaunch {
   }
 };
 
+// RHMC_KERNEL=generic forces the generic kernel (used by the parity tests to
+// cover both code paths on the same inputs).
+bool force_generic() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  return e && std::strcmp(e, "generic") == 0;
+}
+
+template <int IMG>
+int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  int W = 4;
+  size_t lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
+  while (lds > (size_t)ctx->max_lds && W > 1) {
+    W >>= 1;
+    lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
+  }
+  const dim3 grid((unsigned)((a.n_chains + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL(leapfrog_k1_tiled<IMG>, grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s) {
@@ -592,6 +615,29 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
   if (P->counter_max < 1) return fail(RHMC_ERR_ARG, "counter_max < 1");
   if (n_chains == 0) return RHMC_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int side = ctx->rows;
+  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
+      (side == 16 || side == 32 || side == 48 || side == 64)) {
+    LeapArgsK1 t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = d_it;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.n_chains = n_chains;
+    t.n_steps = n_steps;
+    t.rows = ctx->rows;
+    t.cols = ctx->cols;
+    t.pad = 0;
+    t.c = a.c;
+    switch (side) {
+      case 16: return launch_tiled<16>(ctx, t, s);
+      case 32: return launch_tiled<32>(ctx, t, s);
+      case 48: return launch_tiled<48>(ctx, t, s);
+      default: return launch_tiled<64>(ctx, t, s);
+    }
+  }
   size_t lds;
   int W;
   if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;

@@ -94,8 +94,19 @@ def test_trajectory_stepwise(gpu_lib, name, qtol, ptol, horizon):
         assert_state_close(p, Pm[:, s + 1], 1e-10, "%s p step %d" % (name, s))
 
 
+@pytest.fixture(params=["auto", "generic"])
+def kernel_path(request, monkeypatch):
+    """Run a test on the specialised single-star kernel (auto) and again on
+    the generic kernel (RHMC_KERNEL=generic)."""
+    if request.param == "generic":
+        monkeypatch.setenv("RHMC_KERNEL", "generic")
+    else:
+        monkeypatch.delenv("RHMC_KERNEL", raising=False)
+    return request.param
+
+
 @pytest.mark.parametrize("name,qtol,ptol,horizon", TRAJ)
-def test_trajectory_fused(gpu_lib, name, qtol, ptol, horizon):
+def test_trajectory_fused(gpu_lib, kernel_path, name, qtol, ptol, horizon):
     """Free-running: all steps fused in one launch (the production path)."""
     capi = gpu_lib
     z = load_golden(name)
@@ -112,7 +123,7 @@ def test_trajectory_fused(gpu_lib, name, qtol, ptol, horizon):
     assert not (st & capi.STATUS_NONFINITE).any()
 
 
-def test_chains_independent(gpu_lib):
+def test_chains_independent(gpu_lib, kernel_path):
     """A batch gives exactly the per-chain results (no cross-chain coupling)."""
     capi = gpu_lib
     z = load_golden("traj_c2")
@@ -129,7 +140,7 @@ def test_chains_independent(gpu_lib):
         assert np.array_equal(qs, qb[c]) and np.array_equal(ps, pb[c])
 
 
-def test_oracle_matches_gpu_random_chains(gpu_lib):
+def test_oracle_matches_gpu_random_chains(gpu_lib, kernel_path):
     """Seeded random chains at C2 geometry: GPU vs the CPU oracle, 100 steps."""
     capi = gpu_lib
     z = load_golden("traj_c2")

@@ -1,0 +1,118 @@
+// Microbenchmarks for design decisions (not part of the product):
+//   1. accuracy of rcp + 1 Newton step + residual correction vs IEEE fp64 div
+//   2. throughput of IEEE div vs the fast form
+//   3. DPP all-reduce vs __shfl_xor all-reduce (bitwise identical across lanes?)
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+
+__device__ __forceinline__ double fast_div(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  double q = n * r;
+  double res = fma(-d, q, n);
+  return fma(r, res, q);
+}
+__device__ __forceinline__ double fast_div2(double n, double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  double q = n * r;
+  double res = fma(-d, q, n);
+  return fma(r, res, q);
+}
+
+__global__ void acc_kernel(const double* n, const double* d, unsigned long long* bad1,
+                           unsigned long long* bad2, unsigned long long* ulp1, int N) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N) return;
+  double a = n[i] / d[i];
+  double b = fast_div(n[i], d[i]);
+  double c = fast_div2(n[i], d[i]);
+  if (a != b) { atomicAdd(bad1, 1ull); long long x = __double_as_longlong(a) - __double_as_longlong(b); if (x < 0) x = -x; atomicMax(ulp1, (unsigned long long)x); }
+  if (a != c) atomicAdd(bad2, 1ull);
+}
+
+template <int MODE>
+__global__ void thr_kernel(double* out, double seed, int iters) {
+  double acc = 0, d = seed + threadIdx.x * 1e-3, n0 = 3.0 + threadIdx.x;
+  double d1 = d + 1, d2 = d + 2, d3 = d + 3;
+  for (int i = 0; i < iters; ++i) {
+    if (MODE == 0) { acc += n0 / d + n0 / d1 + n0 / d2 + n0 / d3; }
+    else if (MODE == 1) { acc += fast_div(n0, d) + fast_div(n0, d1) + fast_div(n0, d2) + fast_div(n0, d3); }
+    else { acc = fma(acc, 1.0000001, d) ; acc = fma(acc, 0.9999999, d1); acc = fma(acc, 1.0000001, d2); acc = fma(acc, 0.9999999, d3);}
+    d += 1e-9; d1 += 1e-9; d2 += 1e-9; d3 += 1e-9;
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = acc;
+}
+
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v) {
+  long long b = __double_as_longlong(v);
+  int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+  int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double rl(double v, int l) {
+  long long b = __double_as_longlong(v);
+  int lo = __builtin_amdgcn_readlane((int)b, l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__global__ void dpp_kernel(const double* in, double* out) {
+  double v = in[threadIdx.x];
+  v += dpp_d<0xB1>(v);
+  v += dpp_d<0x4E>(v);
+  v += dpp_d<0x141>(v);
+  v += dpp_d<0x140>(v);
+  double s = (rl(v, 0) + rl(v, 16)) + (rl(v, 32) + rl(v, 48));
+  out[threadIdx.x] = s;
+}
+
+int main() {
+  const int N = 1 << 24;
+  std::vector<double> hn(N), hd(N);
+  srand(1);
+  for (int i = 0; i < N; ++i) {
+    hn[i] = (double)(rand() % 5000);                   // Poisson counts
+    hd[i] = 24.98 + 40000.0 * pow((double)rand() / RAND_MAX, 6.0);  // Lambda in [B, B + f*psf]
+  }
+  double *dn, *dd, *dout; unsigned long long* cnt;
+  hipMalloc(&dn, N * 8); hipMalloc(&dd, N * 8); hipMalloc(&cnt, 24); hipMalloc(&dout, 1 << 24);
+  hipMemcpy(dn, hn.data(), N * 8, hipMemcpyHostToDevice);
+  hipMemcpy(dd, hd.data(), N * 8, hipMemcpyHostToDevice);
+  hipMemset(cnt, 0, 24);
+  acc_kernel<<<N / 256, 256>>>(dn, dd, cnt, cnt + 1, cnt + 2, N);
+  unsigned long long h[3];
+  hipMemcpy(h, cnt, 24, hipMemcpyDeviceToHost);
+  printf("fast_div (1 NR + corr): %llu / %d differ from IEEE (max %llu ulp); 2 NR + corr: %llu differ\n", h[0], N, h[2], h[1]);
+
+  hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
+  for (int mode = 0; mode < 3; ++mode) {
+    for (int rep = 0; rep < 2; ++rep) {
+      hipEventRecord(a);
+      if (mode == 0) thr_kernel<0><<<4096, 256>>>(dout, 1.5, 2000);
+      if (mode == 1) thr_kernel<1><<<4096, 256>>>(dout, 1.5, 2000);
+      if (mode == 2) thr_kernel<2><<<4096, 256>>>(dout, 1.5, 2000);
+      hipEventRecord(b); hipEventSynchronize(b);
+      float ms; hipEventElapsedTime(&ms, a, b);
+      double ops = 4096.0 * 256 * 2000 * 4;
+      if (rep) printf("mode %d (%s): %.3f ms, %.1f G ops/s, %.2f SIMD-cycles/wave-op\n", mode,
+                      mode == 0 ? "IEEE div" : mode == 1 ? "fast div" : "fma chain", ms, ops / ms / 1e6,
+                      (ms * 1e-3 * 2.4e9 * 1024) / (ops / 64));
+    }
+  }
+  std::vector<double> hin(64), hout(64);
+  for (int i = 0; i < 64; ++i) hin[i] = sin(i * 1.3) * 1e3;
+  hipMemcpy(dn, hin.data(), 512, hipMemcpyHostToDevice);
+  dpp_kernel<<<1, 64>>>(dn, dout);
+  hipMemcpy(hout.data(), dout, 512, hipMemcpyDeviceToHost);
+  double ref = 0; for (int i = 0; i < 64; ++i) ref += hin[i];
+  bool same = true; for (int i = 1; i < 64; ++i) same &= hout[i] == hout[0];
+  printf("dpp allreduce: lanes identical=%d, value %.17g ref %.17g\n", (int)same, hout[0], ref);
+  return 0;
+}
