@@ -75,7 +75,8 @@ struct Tiled {
   // dphidq at (f, x, y) for the wave's chain (every lane gets the result).
   static __device__ __forceinline__ void gradient(const double* __restrict__ sDl, double* tab,
                                                   double f, double x, double y, const Consts& c,
-                                                  double& gf, double& gx, double& gy) {
+                                                  const LeanConsts& lc, double& gf, double& gx,
+                                                  double& gy) {
     const int lane = lane_id();
     const int ta = lane >> 3, tb = lane & 7;
     // separable PSF factors: lane l < IMG builds row l and column l
@@ -101,18 +102,29 @@ struct Tiled {
     double srow[T], scol[T];
 #pragma unroll
     for (int k = 0; k < T; ++k) srow[k] = scol[k] = 0.0;
+    // Pixels are taken in pairs sharing one v_rcp_f64: 1/(L1 L2) refined by
+    // one Newton step gives 1/L1 = L2/(L1 L2) and 1/L2 = L1/(L1 L2) to ~2^-46,
+    // and the residual correction of fast_div brings each D/L to the
+    // correctly rounded quotient (tools/microbench.hip).
+    static_assert((T * T) % 2 == 0, "pixel pairs");
 #pragma unroll
-    for (int ii = 0; ii < T; ++ii) {
-#pragma unroll
-      for (int jj = 0; jj < T; ++jj) {
-        const double dv = sDl[(ii * T + jj) * 64];
-        const double psf = ex[ii] * ey[jj];
-        const double lam = fma(f, psf, c.B);           // B + f PSF (:373-376)
-        const double r = fast_div(dv, lam);            // D/Lambda (:379)
-        const double w = fma(psf, r, -psf);            // rho * PSF
-        srow[ii] += w;
-        scol[jj] += w;
-      }
+    for (int pp = 0; pp < T * T; pp += 2) {
+      const int i1 = pp / T, j1 = pp % T, i2 = (pp + 1) / T, j2 = (pp + 1) % T;
+      const double d1 = sDl[pp * 64], d2 = sDl[(pp + 1) * 64];
+      const double psf1 = ex[i1] * ey[j1], psf2 = ex[i2] * ey[j2];
+      const double l1 = fma(f, psf1, c.B), l2 = fma(f, psf2, c.B);  // B + f PSF (:373-376)
+      const double L = l1 * l2;
+      double r = __builtin_amdgcn_rcp(L);
+      r = fma(r, fma(-L, r, 1.0), r);
+      const double r1 = l2 * r, r2 = l1 * r;
+      double q1 = d1 * r1, q2 = d2 * r2;                            // D/Lambda (:379)
+      q1 = fma(r1, fma(-l1, q1, d1), q1);
+      q2 = fma(r2, fma(-l2, q2, d2), q2);
+      const double w1 = fma(psf1, q1, -psf1), w2 = fma(psf2, q2, -psf2);  // rho * PSF
+      srow[i1] += w1;
+      scol[j1] += w1;
+      srow[i2] += w2;
+      scol[j2] += w2;
     }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
@@ -128,7 +140,7 @@ struct Tiled {
     gx = -s1 * f / c.var;                              // :405
     gy = -s2 * f / c.var;                              // :406
     if (c.use_prior) gf += c.alpha / f;                // :408-409
-    gf += metric_flux_term(f, c);                      // dphidq (:459-463)
+    gf += metric_flux_term_lean(f, lc);                // dphidq (:459-463)
   }
 };
 
@@ -165,12 +177,13 @@ __global__ void __launch_bounds__(256) leapfrog_k1_tiled(LeapArgsK1 a) {
   double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
   double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
   const double hdt = c.hdt;
+  const LeanConsts lc = lean_consts(c);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
 
   for (int s = 0;; ++s) {
     double gf, gx, gy;
-    TL::gradient(sDl, tab, f, x, y, c, gf, gx, gy);
+    TL::gradient(sDl, tab, f, x, y, c, lc, gf, gx, gy);
     if (s > 0) {
       // (5) closing half kick of step s-1 (:551) and (6) reflection (:554-564)
       pf = pf - hdt * gf;
@@ -198,7 +211,7 @@ __global__ void __launch_bounds__(256) leapfrog_k1_tiled(LeapArgsK1 a) {
 
     // (2) p fixed point on the flux slot (:528-535)
     {
-      const double coef = dtaudq_coef(f, c);
+      const double coef = dtaudq_coef_lean(f, lc);
       const double rho = pf;
       double dp;
       int n = 0;
@@ -214,15 +227,16 @@ __global__ void __launch_bounds__(256) leapfrog_k1_tiled(LeapArgsK1 a) {
     // (3) q fixed point (:538-545)
     {
       const double sf = f, sx = x, sy = y;
-      const double hff0 = H_ff(sf, c), hxx0 = H_xx(sf, c);
-      const double af = pf / hff0, ax = px / hxx0, ay = py / hxx0;
+      double ihff, ihxx;
+      inv_metric(sf, lc, ihff, ihxx);
+      const double af = pf * ihff, ax = px * ihxx, ay = py * ihxx;  // dtaudp(sig, p)
       double dq;
       int n = 0;
       do {
-        const double hff = H_ff(f, c), hxx = H_xx(f, c);
-        const double nf = sf + hdt * (af + pf / hff);
-        const double nx = sx + hdt * (ax + px / hxx);
-        const double ny = sy + hdt * (ay + py / hxx);
+        inv_metric(f, lc, ihff, ihxx);
+        const double nf = sf + hdt * (af + pf * ihff);
+        const double nx = sx + hdt * (ax + px * ihxx);
+        const double ny = sy + hdt * (ay + py * ihxx);
         dq = nanmax2(nanmax2(fabs(f - nf), fabs(x - nx)), fabs(y - ny));
         f = nf;
         x = nx;
@@ -233,7 +247,7 @@ __global__ void __launch_bounds__(256) leapfrog_k1_tiled(LeapArgsK1 a) {
       if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
     }
     // (4) p -= dt/2 dtaudq(q, p) (:548)
-    pf = pf - hdt * ((pf * pf) * dtaudq_coef(f, c) / 2.0);
+    pf = pf - hdt * ((pf * pf) * dtaudq_coef_lean(f, lc) / 2.0);
   }
 
   if (lane == 0) {

@@ -87,6 +87,69 @@ __device__ __forceinline__ double H_xx_grad(double f, const Consts& c) {
   return c.g_xx * a * (1.0 / (s * s));
 }
 
+// ---------------------------------------------------------------------------
+// Division-lean form of the same metric for the single-star kernel.  Every
+// quantity the step needs is a few FMAs of
+//   A  = f/g_ff2 + (B/g0)/g_ff        (= 1/H_ff)
+//   Bf = f + (B/g0)/g_ff              (H_ff' = -1/Bf^2)
+//   u  = 1/max(f, f_low),  s = u/g1 + (B/g2) u^2   (H_xx = g_xx/s)
+// with one reciprocal per evaluation instead of the reference's chain of
+// divides; results agree with the reference expressions to a few ulp.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double rcp_nr(double d) {  // ~correctly rounded 1/d
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
+
+struct LeanConsts {
+  double inv_gff2, c0, inv_g1, Bg2, inv_gxx, f_low;
+};
+
+__device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
+  LeanConsts l;
+  l.inv_gff2 = 1.0 / c.g_ff2;
+  l.c0 = c.c0;
+  l.inv_g1 = 1.0 / c.g1;
+  l.Bg2 = c.B / c.g2;
+  l.inv_gxx = 1.0 / c.g_xx;
+  l.f_low = c.f_low;
+  return l;
+}
+
+// 1/H_ff, 1/H_xx at flux f (the q-loop's dtaudp = p * (1/H)).
+__device__ __forceinline__ void inv_metric(double f, const LeanConsts& l, double& ihff,
+                                           double& ihxx) {
+  ihff = fma(f, l.inv_gff2, l.c0);
+  const double fl = (f < l.f_low) ? l.f_low : f;
+  const double u = rcp_nr(fl);
+  ihxx = (u * fma(l.Bg2, u, l.inv_g1)) * l.inv_gxx;
+}
+
+// -H_ff'/H_ff^2 = (A/Bf)^2  (dtaudq's coefficient, :479)
+__device__ __forceinline__ double dtaudq_coef_lean(double f, const LeanConsts& l) {
+  const double A = fma(f, l.inv_gff2, l.c0);
+  const double t = A * rcp_nr(f + l.c0);
+  return t * t;
+}
+
+// (H_ff'/H_ff + 2 H_xx'/H_xx)/2 with H_ff'/H_ff = -A/Bf^2 and
+// H_xx'/H_xx = u^2 (1/g1 + 2 (B/g2) u)/s (0 when clamped) (:461-463)
+__device__ __forceinline__ double metric_flux_term_lean(double f, const LeanConsts& l) {
+  const double A = fma(f, l.inv_gff2, l.c0);
+  const double ib = rcp_nr(f + l.c0);
+  const double t1 = -A * (ib * ib);
+  double t2 = 0.0;
+  if (!(f < l.f_low)) {
+    const double u = rcp_nr(f);
+    const double s = u * fma(l.Bg2, u, l.inv_g1);
+    t2 = (u * u) * fma(2.0 * l.Bg2, u, l.inv_g1) * rcp_nr(s);
+  }
+  return (t1 + 2.0 * t2) / 2.0;
+}
+
 // dphidq's metric term on the flux slot: (H_ff'/H_ff + 2 H_xx'/H_xx)/2 (:461-463)
 __device__ __forceinline__ double metric_flux_term(double f, const Consts& c) {
   const double hff = H_ff(f, c), hffg = H_ff_grad(f, c);

@@ -1,0 +1,449 @@
+"""The reference's `sampler_RHMC` entry points, routed to the MI355X engine.
+
+Mirrors jaekor91/HMC-stellar-toy-model `sampler_RHMC.py` (file:line cited per
+method): same class names, constructor arguments, attributes (set them after
+construction exactly like the reference scripts do, e.g.
+`gym.num_rows = gym.num_cols = 32; gym.use_prior = True`), method names,
+argument meaning, global-NumPy-RNG draw order and return values.
+
+What runs where:
+  * RHMC_single_step, dVdq, dphidq, V and the batched RHMC_steps run in
+    librhmc.so (HIP kernels, rhmc_amd.capi).  There is no CPU fallback:
+    without a GPU these raise.
+  * O(K) scalar helpers (H, H_ff, H_xx, T, dtaudq, dtaudp, dVdq_RHMC) and the
+    MH bookkeeping stay on the host, as NumPy, like in the reference.
+
+Quirks kept on purpose: g0/g1/g2 are computed once at
+construction on the default 48x48 grid and NOT recomputed when num_rows is
+changed later; single_gym ignores its g_ff2 argument; V needs fmin/fmax for
+its prior constant (computed and cached on the first V call); use_Vc needs
+f_expnt to be set (TypeError otherwise, like the reference).
+
+Out of scope here: plotting (display_image, diagnostics_*) and
+the reversible-jump birth/death/split/merge moves (P_move[1:] must be 0).
+"""
+import numpy as np
+
+from . import capi
+from .photometry import (default_exp_setup, factors, flux2mag, gauss_PSF, mag2flux,
+                         poisson_realization)
+
+
+class base_class(object):
+    """sampler_RHMC.py:27-566."""
+
+    def __init__(self, dt=1., g_xx=10, g_ff=10, g_ff2=2):
+        self._D = None
+        self._ctx = None
+        self._ctx_shape = None
+        self.M = None
+        (self.num_rows, self.num_cols, self.flux_to_count, self.PSF_FWHM_pix,
+         self.B_count, self.arcsec_to_pix, self.mB, self.f_lim) = default_exp_setup()
+        self.dt = dt
+        self.g_xx = g_xx
+        self.g_ff = g_ff
+        self.g_ff2 = g_ff2
+        self.compute_factors()
+        self.vmin = None
+        self.vmax = None
+        self.use_prior = False
+        self.alpha = 2.
+        self.use_Vc = False
+        self.beta = 1.
+        self.f_expnt = None
+        self.Vc_r_pow = 1.
+        self.V_prior_const = None
+        self.K_split = 1.
+        self.beta_a = 2.
+        self.beta_b = 2.
+        self.move_types = {0: "within", 1: "birth", 2: "death", 3: "split", 4: "merge"}
+        self.device = 0
+
+    # ---------------------------------------------------------------- data
+    @property
+    def D(self):
+        return self._D
+
+    @D.setter
+    def D(self, value):
+        self._D = None if value is None else np.ascontiguousarray(value, dtype=np.float64)
+        self._ctx_shape = None        # re-upload on next use
+
+    def _context(self):
+        if self._D is None:
+            raise ValueError("no data image: call gen_mock_data() or set .D first")
+        if self._ctx is None:
+            self._ctx = capi.Context(self._D, device=self.device)
+        elif self._ctx_shape is None:
+            self._ctx.set_image(self._D)
+        self._ctx_shape = self._D.shape
+        return self._ctx
+
+    def _params(self, delta=1e-6, counter_max=1000, for_energy=False):
+        vpc = 0.
+        if for_energy:
+            if self.V_prior_const is None:     # :320-321 (evaluated unconditionally)
+                self.V_prior_const = np.log(self.num_rows * self.num_cols) - np.log(
+                    (1 - self.alpha) / (self.fmax ** (1 - self.alpha) - self.fmin ** (1 - self.alpha)))
+            vpc = self.V_prior_const
+        if self.use_Vc and self.f_expnt is None:
+            # the reference raises here too (:388, None ** ... TypeError)
+            raise TypeError("use_Vc requires f_expnt to be set")
+        return capi.make_params(
+            dt=self.dt, delta=delta, counter_max=counter_max, B_count=self.B_count,
+            f_lim=self.f_lim, f_low=self.mag2flux_converter(self.mB + 2),
+            fwhm_pix=self.PSF_FWHM_pix, g_xx=self.g_xx, g_ff=self.g_ff, g_ff2=self.g_ff2,
+            g0=self.g0, g1=self.g1, g2=self.g2, use_prior=self.use_prior, alpha=self.alpha,
+            use_Vc=self.use_Vc, beta=self.beta, Vc_r_pow=self.Vc_r_pow, V_prior_const=vpc)
+
+    def _check_geometry(self):
+        if self._D is not None and self._D.shape != (self.num_rows, self.num_cols):
+            raise ValueError("D has shape %s but num_rows/num_cols are %d/%d"
+                             % (self._D.shape, self.num_rows, self.num_cols))
+
+    def gen_mock_data(self, q_true=None, return_data=False):
+        """sampler_RHMC.py:77-99 (global NumPy RNG, row-major Poisson draws)."""
+        data = np.ones((self.num_rows, self.num_cols), dtype=float) * self.B_count
+        for i in range(q_true.shape[0]):
+            mag, x, y = q_true[i]
+            data += self.mag2flux_converter(mag) * gauss_PSF(
+                self.num_rows, self.num_cols, x, y, FWHM=self.PSF_FWHM_pix)
+        data = poisson_realization(data)
+        if return_data:
+            return data
+        self.D = data
+
+    def gen_model(self, q_model):
+        """sampler_RHMC.py:101-116."""
+        model = np.ones((self.num_rows, self.num_cols), dtype=float) * self.B_count
+        for i in range(q_model.shape[0]):
+            mag, x, y = q_model[i]
+            model += self.mag2flux_converter(mag) * gauss_PSF(
+                self.num_rows, self.num_cols, x, y, FWHM=self.PSF_FWHM_pix)
+        return model
+
+    def gen_noise_profile(self, q_true, N_trial=1000, sig_fac=10):
+        """sampler_RHMC.py:118-145 (`normed=` is NumPy's `density=` today)."""
+        truth = self.gen_model(q_true)
+        res = np.vstack([poisson_realization(truth) - truth for _ in range(N_trial)]).ravel()
+        sig = np.sqrt(self.B_count)
+        bins = np.arange(-sig_fac * sig, sig_fac * sig, sig / 5.)
+        hist, _ = np.histogram(res, bins=bins, density=True)
+        self.hist_noise = hist
+        self.centers_noise = (bins[1:] + bins[:-1]) / 2.
+
+    def mag2flux_converter(self, mag):
+        """sampler_RHMC.py:147-152"""
+        return mag2flux(mag) * self.flux_to_count
+
+    def flux2mag_converter(self, flux):
+        """sampler_RHMC.py:154-159"""
+        return flux2mag(flux / self.flux_to_count)
+
+    def compute_factors(self):
+        """sampler_RHMC.py:161-167 (on the grid current at call time)."""
+        self.g0, self.g1, self.g2 = factors(self.num_rows, self.num_cols, self.num_rows / 2.,
+                                            self.num_cols / 2., self.PSF_FWHM_pix)
+
+    def default_exp_setup(self):
+        """sampler_RHMC.py:169-201"""
+        r, c, ftc, fwhm, B, a2p, mB, f_lim = default_exp_setup()
+        self.mB, self.f_lim = mB, f_lim
+        return r, c, ftc, fwhm, B, a2p
+
+    def u_sample(self, d):
+        """sampler_RHMC.py:203-207"""
+        return np.random.randn(d)
+
+    def format_q(self, q):
+        """sampler_RHMC.py:209-217 (mutates q like the reference)."""
+        for i in range(q.shape[0]):
+            q[i, 0] = self.mag2flux_converter(q[i, 0])
+        return q.reshape((q.size,))
+
+    def reverse_format_q(self, q):
+        """sampler_RHMC.py:219-227"""
+        q = np.copy(q.reshape((-1, 3)))
+        for i in range(q.shape[0]):
+            q[i, 0] = self.flux2mag_converter(q[i, 0])
+        return q
+
+    # ---------------------------------------------------- O(K) host helpers
+    def H(self, q, grad=False):
+        """sampler_RHMC.py:229-258"""
+        K = q.size // 3
+        Hd = np.zeros(q.size)
+        Hg = np.zeros(q.size)
+        for i in range(K):
+            f = q[3 * i]
+            if grad:
+                Hd[3 * i], Hg[3 * i] = self.H_ff(f, grad=True)
+                v, g = self.H_xx(f, grad=True)
+                Hd[3 * i + 1] = Hd[3 * i + 2] = v
+                Hg[3 * i + 1] = Hg[3 * i + 2] = g
+            else:
+                Hd[3 * i] = self.H_ff(f)
+                Hd[3 * i + 1] = Hd[3 * i + 2] = self.H_xx(f)
+        return (Hd, Hg) if grad else Hd
+
+    def H_xx(self, f, grad=False):
+        """sampler_RHMC.py:260-280"""
+        f_low = self.mag2flux_converter(self.mB + 2)
+        low = f < f_low
+        if low:
+            f = f_low
+        s = 1. / (self.g1 * f) + self.B_count / (self.g2 * f ** 2)
+        val = self.g_xx * s ** -1
+        if not grad:
+            return val
+        g = 0 if low else self.g_xx * (1. / (self.g1 * f ** 2) + 2 * self.B_count
+                                       / (self.g2 * f ** 3)) * s ** -2
+        return val, g
+
+    def H_ff(self, f, grad=False):
+        """sampler_RHMC.py:283-292 (gradient ignores g_ff2, :292)"""
+        val = 1. / (f / self.g_ff2 + (self.B_count / self.g0) / self.g_ff)
+        if not grad:
+            return val
+        return val, -1. / (f + (self.B_count / self.g0) / self.g_ff) ** 2
+
+    def T(self, p, H_diag):
+        """sampler_RHMC.py:353-363"""
+        return (np.sum(p ** 2 / H_diag) + np.sum(np.log(np.abs(H_diag)))) / 2.
+
+    def dVdq_RHMC(self, q, p):
+        """sampler_RHMC.py:427-446"""
+        g = np.zeros_like(q)
+        H, Hg = self.H(q, grad=True)
+        for i in range(q.size // 3):
+            t1 = (p[3 * i] ** 2) * (-Hg[3 * i] / H[3 * i] ** 2)
+            t2 = (Hg[3 * i] / H[3 * i]) + (2 * Hg[3 * i + 1] / H[3 * i + 1])
+            g[3 * i] = (t1 + t2) / 2.
+        return g
+
+    def dtaudq(self, q, p):
+        """sampler_RHMC.py:467-483"""
+        g = np.zeros_like(q)
+        H, Hg = self.H(q, grad=True)
+        for i in range(q.size // 3):
+            g[3 * i] = ((p[3 * i] ** 2) * (-Hg[3 * i] / H[3 * i] ** 2)) / 2.
+        return g
+
+    def dtaudp(self, q, p):
+        """sampler_RHMC.py:485-492"""
+        return p / self.H(q, grad=False)
+
+    # ---------------------------------------------------- device hot path
+    def V(self, q, f_pos=False):
+        """sampler_RHMC.py:294-351 on the GPU (rhmc_energy).  q: [3K] or [n, 3K]."""
+        self._check_geometry()
+        V, _ = self._context().energy(self._params(for_energy=True), q, None, f_pos=f_pos)
+        return V
+
+    def V_T(self, q, p, f_pos=False):
+        """Batched V(q) and T(p, H(q)) in one launch: q, p [n, 3K] -> (V[n], T[n])."""
+        self._check_geometry()
+        return self._context().energy(self._params(for_energy=True), q, p, f_pos=f_pos)
+
+    def dVdq(self, q):
+        """sampler_RHMC.py:365-425 on the GPU (rhmc_gradient kind 0)."""
+        self._check_geometry()
+        return self._context().gradient(self._params(), q, kind=0)
+
+    def dphidq(self, q):
+        """sampler_RHMC.py:448-465 on the GPU (rhmc_gradient kind 1)."""
+        self._check_geometry()
+        return self._context().gradient(self._params(), q, kind=1)
+
+    def RHMC_single_step(self, q_tmp, p_tmp, delta=1e-6, counter_max=1000):
+        """sampler_RHMC.py:522-566 — one implicit generalized-leapfrog step with
+        flux-wall / edge reflection.  Returns new (q, p); inputs untouched."""
+        return self.RHMC_steps(q_tmp, p_tmp, 1, delta=delta, counter_max=counter_max)
+
+    def RHMC_steps(self, q, p, n_steps, delta=1e-6, counter_max=1000, return_info=False):
+        """Batched, fused: n_steps RHMC_single_step()s on every chain of
+        q, p [n_chains, 3K] (or [3K]) in one launch.  With return_info also
+        returns the per-chain (p-loop, q-loop) iteration sums and status bits."""
+        self._check_geometry()
+        return self._context().leapfrog(self._params(delta, counter_max), q, p, n_steps,
+                                        return_info=return_info)
+
+    def display_image(self, *args, **kwargs):
+        raise NotImplementedError("plotting is out of scope of the MI355X engine")
+
+
+class single_gym(base_class):
+    """sampler_RHMC.py:569-879 (single trajectories)."""
+
+    def __init__(self, Nsteps=100, dt=0.1, g_xx=1., g_ff=1., g_ff2=1.):
+        base_class.__init__(self, dt=dt, g_xx=g_xx, g_ff=g_ff, g_ff2=1.)  # g_ff2 ignored (:578)
+        self.Nsteps = Nsteps
+        self.q_chain = self.p_chain = self.E_chain = self.V_chain = self.T_chain = None
+
+    def run_single_HMC(self, q_model_0=None, f_pos=False):
+        """sampler_RHMC.py:592-647 — plain HMC, naive leapfrog, unit metric."""
+        self.Nobjs = q_model_0.shape[0]
+        self.d = self.Nobjs * 3
+        q_model_0 = self.format_q(q_model_0)
+        n = self.Nsteps + 1
+        self.q_chain = np.zeros((n, self.d))
+        self.p_chain = np.zeros((n, self.d))
+        self.E_chain = np.zeros(n)
+        self.V_chain = np.zeros(n)
+        self.T_chain = np.zeros(n)
+        q_tmp = q_model_0
+        p_tmp = self.u_sample(self.d)
+        self.q_chain[0], self.p_chain[0] = q_tmp, p_tmp
+        self.V_chain[0] = self.V(q_tmp, f_pos=f_pos)
+        self.T_chain[0] = self.T(p_tmp, np.ones_like(p_tmp))
+        self.E_chain[0] = self.V_chain[0] + self.T_chain[0]
+        for i in range(1, n):
+            p_half = p_tmp - self.dt * self.dVdq(q_tmp) / 2.
+            q_tmp = q_tmp + self.dt * p_half
+            p_tmp = p_half - self.dt * self.dVdq(q_tmp) / 2.
+            self.q_chain[i], self.p_chain[i] = q_tmp, p_tmp
+            self.V_chain[i] = self.V(q_tmp, f_pos=f_pos)
+            self.T_chain[i] = self.T(p_tmp, np.ones_like(p_tmp))
+            self.E_chain[i] = self.V_chain[i] + self.T_chain[i]
+
+    def run_single_RHMC(self, q_model_0=None, f_pos=False, solver="naive", delta=1e-6,
+                        p_initial=None, counter_max=100):
+        """sampler_RHMC.py:649-783.  solver="implicit" is the engine's step
+        (identical math to RHMC_single_step, :729-772); "naive" and
+        "leap_frog" use the device gradient with host metric terms."""
+        if solver not in ("naive", "leap_frog", "implicit"):
+            assert False
+        self.Nobjs = q_model_0.shape[0]
+        self.d = self.Nobjs * 3
+        q_model_0 = self.format_q(q_model_0)
+        n = self.Nsteps + 1
+        self.q_chain = np.zeros((n, self.d))
+        self.p_chain = np.zeros((n, self.d))
+        self.E_chain = np.zeros(n)
+        self.V_chain = np.zeros(n)
+        self.T_chain = np.zeros(n)
+        q_tmp = q_model_0
+        H_diag = self.H(q_tmp)
+        if p_initial is None:
+            p_initial = self.u_sample(self.d) * np.sqrt(H_diag)
+        p_tmp = p_initial
+        self.q_chain[0], self.p_chain[0] = q_tmp, p_tmp
+        V0 = self.V(q_tmp, f_pos=f_pos)
+        T0 = self.T(p_tmp, H_diag)
+        for i in range(1, n):
+            if solver == "implicit":
+                q_tmp, p_tmp = self.RHMC_single_step(q_tmp, p_tmp, delta=delta,
+                                                     counter_max=counter_max)
+                H_diag = self.H(q_tmp)
+            elif solver == "naive":
+                q_new = q_tmp + self.dt * p_tmp / H_diag
+                p_old = p_tmp
+                p_tmp = p_tmp - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_tmp))
+                if f_pos:
+                    for k in range(self.Nobjs):
+                        if q_new[3 * k] < self.f_lim:
+                            p_tmp[3 * k] = p_old[3 * k] * -1.
+                q_tmp = q_new
+                H_diag = self.H(q_tmp)
+            else:  # leap_frog
+                p_half = p_tmp - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_tmp)) / 2.
+                q_tmp = q_tmp + self.dt * p_half / H_diag
+                p_tmp = p_half - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_half)) / 2.
+                if f_pos:
+                    for k in range(self.Nobjs):
+                        if q_tmp[3 * k] < self.f_lim:
+                            p_tmp[3 * k] = p_half[3 * k] * -1.
+                H_diag = self.H(q_tmp)
+            self.q_chain[i], self.p_chain[i] = q_tmp, p_tmp
+            self.V_chain[i] = self.V(q_tmp, f_pos=f_pos) - V0
+            self.T_chain[i] = self.T(p_tmp, H_diag) - T0
+            self.E_chain[i] = self.V_chain[i] + self.T_chain[i]
+
+
+class multi_gym(base_class):
+    """sampler_RHMC.py:883-1473 (fixed-dimension RHMC MCMC)."""
+
+    def __init__(self, Nsteps=100, dt=0.1, g_xx=1., g_ff=1., g_ff2=1.):
+        base_class.__init__(self, dt=dt, g_xx=g_xx, g_ff=g_ff, g_ff2=g_ff2)
+        self.Nsteps = Nsteps
+        self.q_chain = self.p_chain = self.E_chain = self.V_chain = self.T_chain = None
+        self.A_chain = None
+        self.fmin = None
+        self.fmax = None
+
+    def run_RHMC(self, q_model_0, f_pos=True, delta=1e-6, Niter=100, Nsteps=100, dt=1e-1,
+                 save_traj=False, counter_max=1000, verbose=False, q_true=None,
+                 schedule_g_ff2=None, N_max=50, P_move=[1., 0., 0.], schedule_beta=None):
+        """sampler_RHMC.py:937-1198, move-0 ("within") branch.  The Nsteps
+        leapfrog steps of an iteration are ONE fused launch.  Same global
+        NumPy RNG order per iteration as the reference: randn(d), choice
+        (one uniform), random(1)."""
+        if save_traj:
+            assert False                                  # :966-968
+        if P_move[1] != 0 or P_move[2] != 0:
+            raise NotImplementedError("reversible-jump moves are out of scope (P_move[1:] != 0)")
+        self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
+        self.save_traj, self.P_move, self.N_max = save_traj, P_move, N_max
+        self.Nobjs = q_model_0.shape[0]
+        self.d = self.Nobjs * 3
+        q_model_0 = self.format_q(q_model_0)
+        self.q_chain = np.zeros((Niter + 1, N_max * 3))
+        self.p_chain = np.zeros((Niter + 1, N_max * 3))
+        self.E_chain = np.zeros(Niter + 1)
+        self.V_chain = np.zeros(Niter + 1)
+        self.T_chain = np.zeros(Niter + 1)
+        self.A_chain = np.zeros(Niter + 1, dtype=bool)
+        self.move_chain = np.zeros(Niter + 1, dtype=int)
+        self.N_chain = np.zeros(Niter + 1, dtype=int)
+        q_tmp = np.copy(q_model_0)
+        for l in range(Niter + 1):
+            if schedule_g_ff2 is not None and l < schedule_g_ff2.size:
+                self.g_ff2 = schedule_g_ff2[l]
+            if schedule_beta is not None and l < schedule_beta.size:
+                self.beta = schedule_beta[l]
+            H_diag = self.H(q_tmp, grad=False)
+            p_tmp = self.u_sample(self.d) * np.sqrt(H_diag)
+            V_initial = self.V(q_tmp, f_pos=f_pos)
+            T_initial = self.T(p_tmp, H_diag)
+            E_initial = V_initial + T_initial
+            self.q_chain[l, :self.d] = q_tmp
+            self.p_chain[l, :self.d] = p_tmp
+            self.V_chain[l] = V_initial
+            self.E_chain[l] = E_initial
+            self.T_chain[l] = T_initial
+            self.N_chain[l] = self.Nobjs
+            move_type = np.random.choice([0, 1, 2], p=self.P_move, size=1)[0]
+            self.move_chain[l] = 0
+            q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
+                                           counter_max=counter_max)
+            H_diag = self.H(q_tmp, grad=False)
+            E_final = self.V(q_tmp, f_pos=f_pos) + self.T(p_tmp, H_diag)
+            dE = E_final - E_initial
+            lnu = np.log(np.random.random(1))
+            if (dE < 0) or (lnu < -dE):
+                self.A_chain[l] = 1
+            else:
+                q_tmp = self.q_chain[l, :self.d]
+            if verbose and (l % 50) == 0:
+                print("/---- Completed iteration %d" % l)
+                print("N_objs: %d\n" % self.Nobjs)
+                self.R_accept_report(idx_iter=l, run_window=10)
+        print("Finished. Final report.")                  # :1195-1196
+        self.R_accept_report(idx_iter=-1, running=False)
+
+    def R_accept_report(self, idx_iter, cumulative=True, running=True, run_window=10):
+        """sampler_RHMC.py:1447-1473"""
+        def rep(A, M):
+            for i in range(5):
+                b = M == i
+                n = np.sum(b)
+                if n > 0:
+                    a = np.sum(A[b])
+                    print("%10s: %.2f%% (%d / %d)" % (self.move_types[i], a / float(n) * 100, a, n))
+        if cumulative:
+            print("/--Acceptance rate (cumulative)")
+            rep(self.A_chain[:idx_iter], self.move_chain[:idx_iter])
+        if running:
+            print("/--Acceptance rate (running: %d)" % run_window)
+            rep(self.A_chain[idx_iter - run_window:idx_iter],
+                self.move_chain[idx_iter - run_window:idx_iter])

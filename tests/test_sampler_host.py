@@ -1,0 +1,81 @@
+"""CPU tests of the sampler mirror's host-side pieces (no GPU needed): the
+constructor state, the O(K) metric helpers and the data generation match the
+reference goldens; device-backed methods refuse to run without a GPU instead
+of falling back to the CPU."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from oracle import rhmc_ref as R
+
+
+def _gym_from(par, cls="multi"):
+    from rhmc_amd import sampler
+    g = (sampler.multi_gym if cls == "multi" else sampler.single_gym)(
+        dt=par["dt"], g_xx=par["g_xx"], g_ff=par["g_ff"], g_ff2=par["g_ff2"])
+    g.num_rows, g.num_cols = int(par["rows"]), int(par["cols"])
+    g.use_prior = bool(par["use_prior"])
+    g.alpha = par["alpha"]
+    g.use_Vc = bool(par["use_Vc"])
+    g.beta, g.Vc_r_pow = par["beta"], par["Vc_r_pow"]
+    g.fmin, g.fmax = par["fmin"], par["fmax"]
+    return g
+
+
+def test_constructor_constants_match_reference():
+    from rhmc_amd import sampler
+    z = load_golden("functions")
+    par = R.params_from_npz(z, "k1/par_")
+    g = sampler.multi_gym(g_xx=1., g_ff=1., g_ff2=1.)
+    for k, a in (("B_count", "B_count"), ("f_lim", "f_lim"), ("g0", "g0"), ("g1", "g1"),
+                 ("g2", "g2"), ("fwhm_pix", "PSF_FWHM_pix"), ("flux_to_count", "flux_to_count")):
+        assert getattr(g, a) == par[k], k
+    assert g.num_rows == g.num_cols == 48 and g.mB == 23
+    s = sampler.single_gym(g_ff2=7.)
+    assert s.g_ff2 == 1.                         # single_gym ignores g_ff2 (:578)
+
+
+@pytest.mark.parametrize("name", ["k1", "k1gff2", "k10", "vc5"])
+def test_host_metric_helpers(name):
+    z = load_golden("functions")
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym_from(par)
+    for i, (q, p) in enumerate(zip(z[name + "/q"], z[name + "/p"])):
+        np.testing.assert_array_equal(g.H(q), z[name + "/H"][i])
+        hv, hg = g.H(q, grad=True)
+        np.testing.assert_array_equal(hv, z[name + "/Hv"][i])
+        np.testing.assert_array_equal(hg, z[name + "/Hg"][i])
+        np.testing.assert_array_equal(g.dtaudq(q, p), z[name + "/dtaudq"][i])
+        np.testing.assert_array_equal(g.dtaudp(q, p), z[name + "/dtaudp"][i])
+        np.testing.assert_allclose(g.T(p, g.H(q)), z[name + "/T"][i], rtol=1e-15)
+
+
+def test_gen_mock_data_matches_reference_rng_stream():
+    """gen_mock_data draws the same Poisson stream as the reference."""
+    from rhmc_amd import sampler
+    z = load_golden("functions")
+    g = sampler.multi_gym(g_xx=1., g_ff=1., g_ff2=1.)
+    np.random.seed(77)
+    g.gen_mock_data(np.array([[19., 24.3, 23.8]]))
+    np.testing.assert_array_equal(g.D, z["k1/D"])
+
+
+def test_format_q_roundtrip():
+    from rhmc_amd import sampler
+    g = sampler.multi_gym()
+    stars = np.array([[19., 24.3, 23.8], [21., 3., 4.]])
+    q = g.format_q(stars.copy())
+    np.testing.assert_allclose(g.reverse_format_q(q), stars, rtol=1e-13)
+
+
+def test_quirk_errors_like_reference():
+    from rhmc_amd import sampler
+    g = sampler.multi_gym()
+    g.use_Vc = True                               # f_expnt is None -> TypeError (:388)
+    with pytest.raises(TypeError):
+        g._params()
+    g2 = sampler.multi_gym()
+    with pytest.raises(TypeError):                # fmin/fmax None -> TypeError (:321)
+        g2._params(for_energy=True)
+    with pytest.raises(NotImplementedError):
+        g2.run_RHMC(np.array([[19., 24., 24.]]), P_move=[0.6, 0.2, 0.2])

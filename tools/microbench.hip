@@ -27,6 +27,24 @@ __device__ __forceinline__ double fast_div2(double n, double d) {
   return fma(r, res, q);
 }
 
+__device__ __forceinline__ void pair_div(double d1, double l1, double d2, double l2, double& q1, double& q2) {
+  const double L = l1 * l2;
+  double r = __builtin_amdgcn_rcp(L);
+  r = fma(r, fma(-L, r, 1.0), r);
+  const double r1 = l2 * r, r2 = l1 * r;
+  q1 = d1 * r1; q2 = d2 * r2;
+  q1 = fma(r1, fma(-l1, q1, d1), q1);
+  q2 = fma(r2, fma(-l2, q2, d2), q2);
+}
+__global__ void pair_kernel(const double* n, const double* d, unsigned long long* bad, int N) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (2 * i + 1 >= N) return;
+  double q1, q2;
+  pair_div(n[2*i], d[2*i], n[2*i+1], d[2*i+1], q1, q2);
+  if (q1 != n[2*i] / d[2*i]) atomicAdd(bad, 1ull);
+  if (q2 != n[2*i+1] / d[2*i+1]) atomicAdd(bad, 1ull);
+}
+
 __global__ void acc_kernel(const double* n, const double* d, unsigned long long* bad1,
                            unsigned long long* bad2, unsigned long long* ulp1, int N) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -89,6 +107,11 @@ int main() {
   acc_kernel<<<N / 256, 256>>>(dn, dd, cnt, cnt + 1, cnt + 2, N);
   unsigned long long h[3];
   hipMemcpy(h, cnt, 24, hipMemcpyDeviceToHost);
+  hipMemset(cnt, 0, 8);
+  pair_kernel<<<N / 512, 256>>>(dn, dd, cnt, N);
+  unsigned long long hp;
+  hipMemcpy(&hp, cnt, 8, hipMemcpyDeviceToHost);
+  printf("pair-shared rcp div: %llu / %d differ from IEEE\n", hp, N);
   printf("fast_div (1 NR + corr): %llu / %d differ from IEEE (max %llu ulp); 2 NR + corr: %llu differ\n", h[0], N, h[2], h[1]);
 
   hipEvent_t a, b; hipEventCreate(&a); hipEventCreate(&b);
