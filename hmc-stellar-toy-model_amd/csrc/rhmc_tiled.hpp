@@ -43,16 +43,40 @@ __device__ __forceinline__ double dpp_move(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// gfx950 v_permlane{16,32}_swap on both 32-bit halves of a double, called
+// with the same register as both operands: returns (a, b) such that a + b
+// adds row r to row r^1 (16) or half h to half h^1 (32), with the SAME
+// operand order in both partner rows.
+template <bool SWAP32>
+__device__ __forceinline__ double swap_add(double v) {
+  const long long bits = __double_as_longlong(v);
+  const unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+  unsigned a_lo, b_lo, a_hi, b_hi;
+  if (SWAP32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a_lo = l[0]; b_lo = l[1]; a_hi = h[0]; b_hi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a_lo = l[0]; b_lo = l[1]; a_hi = h[0]; b_hi = h[1];
+  }
+  const double a = __longlong_as_double(((long long)a_hi << 32) | a_lo);
+  const double b = __longlong_as_double(((long long)b_hi << 32) | b_lo);
+  return a + b;
+}
+
 // All-reduce over the wave: xor-1 / xor-2 quad permutes, half-mirror and
-// mirror inside each 16-lane row (every lane of a row ends with the same
-// bits: each step adds two values commutatively), then the 4 row sums in a
-// fixed order.  Deterministic and identical in every lane.
+// mirror inside each 16-lane row (partners add the same two values, so every
+// lane of a row holds the same bits), then row pairs and half pairs by the
+// permlane swaps.  Deterministic and bit-identical in every lane.
 __device__ __forceinline__ double wave_sum_dpp(double v) {
   v += dpp_move<0xB1>(v);   // quad_perm [1,0,3,2]
   v += dpp_move<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_move<0x141>(v);  // row_half_mirror
   v += dpp_move<0x140>(v);  // row_mirror
-  return (bcast(v, 0) + bcast(v, 16)) + (bcast(v, 32) + bcast(v, 48));
+  v = swap_add<false>(v);   // rows 0+1, 2+3
+  return swap_add<true>(v); // (0+1) + (2+3)
 }
 
 template <int IMG>
@@ -83,9 +107,9 @@ struct Tiled {
     if (lane < IMG) {
       const double v = (lane + 0.5) - x;
       const double u = (lane + 0.5) - y;
-      tab[2 * lane] = exp(-(v * v) / c.two_sig2);
+      tab[2 * lane] = exp(-(v * v) * lc.inv_two_sig2);
       tab[2 * lane + 1] = ((double)lane - x) + 0.5;
-      tab[2 * IMG + 2 * lane] = exp(-(u * u) / c.two_sig2) / c.psf_norm;
+      tab[2 * IMG + 2 * lane] = exp(-(u * u) * lc.inv_two_sig2) * lc.inv_norm;
       tab[2 * IMG + 2 * lane + 1] = ((double)lane - y) + 0.5;
     }
     wave_lds_sync();
@@ -137,9 +161,9 @@ struct Tiled {
     const double s1 = wave_sum_dpp(a1);
     const double s2 = wave_sum_dpp(a2);
     gf = -s0;                                          // :404
-    gx = -s1 * f / c.var;                              // :405
-    gy = -s2 * f / c.var;                              // :406
-    if (c.use_prior) gf += c.alpha / f;                // :408-409
+    gx = -s1 * f * lc.inv_var;                         // :405
+    gy = -s2 * f * lc.inv_var;                         // :406
+    if (c.use_prior) gf += c.alpha * rcp_nr(f);        // :408-409
     gf += metric_flux_term_lean(f, lc);                // dphidq (:459-463)
   }
 };
@@ -155,8 +179,11 @@ struct LeapArgsK1 {
   Consts c;
 };
 
+// 4 waves per SIMD (<= 128 VGPRs) lets a 4096-chain launch be resident in
+// one round on 256 CUs; IMG = 64 needs more registers than that.
 template <int IMG>
-__global__ void __launch_bounds__(256) leapfrog_k1_tiled(LeapArgsK1 a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(IMG <= 48 ? 4 : 2)))
+leapfrog_k1_tiled(LeapArgsK1 a) {
   using TL = Tiled<IMG>;
   extern __shared__ double lds[];
   const Consts& c = a.c;

@@ -106,6 +106,7 @@ __device__ __forceinline__ double rcp_nr(double d) {  // ~correctly rounded 1/d
 
 struct LeanConsts {
   double inv_gff2, c0, inv_g1, Bg2, inv_gxx, f_low;
+  double inv_two_sig2, inv_norm, inv_var;  // PSF exponent / normalisation, 1/var
 };
 
 __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
@@ -116,6 +117,9 @@ __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
   l.Bg2 = c.B / c.g2;
   l.inv_gxx = 1.0 / c.g_xx;
   l.f_low = c.f_low;
+  l.inv_two_sig2 = 1.0 / c.two_sig2;
+  l.inv_norm = 1.0 / c.psf_norm;
+  l.inv_var = 1.0 / c.var;
   return l;
 }
 
