@@ -88,14 +88,16 @@ def cpu_baseline(wl, seconds_target=15.0):
                       % (len(jobs), nsteps, wl.name, model)}
 
 
-def load_traffic(workload):
-    """HBM bytes per launch measured by rocprofv3 PMC (profiles/pmc_<wl>.json)."""
+def load_pmc(workload):
+    """rocprofv3 PMC summary of the dominant kernel (profiles/pmc_<wl>.json,
+    written by scripts/pmc_summary.py): HBM bytes per launch and executed
+    fp64 flops per chain-step."""
     path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload.lower())
     try:
         with open(path) as fh:
-            return json.load(fh).get("hbm_bytes_per_launch")
+            return json.load(fh)
     except (OSError, ValueError):
-        return None
+        return {}
 
 
 def main():
@@ -104,7 +106,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="C2")
-    ap.add_argument("--chains", type=int, default=None, help="chains per GPU")
+    ap.add_argument("--chains", type=int, default=None, help="chains per GPU (weak scaling)")
+    ap.add_argument("--global-chains", type=int, default=None,
+                    help="total chains split over the ranks (strong scaling, e.g. C4 = 2^20)")
     ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
     ap.add_argument("--no-cpu", action="store_true")
     args = ap.parse_args()
@@ -113,8 +117,14 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
-    from rhmc_amd import workloads
-    wl = workloads.make(args.workload, n_chains=args.chains, seed_offset=rank)
+    from rhmc_amd import shard, workloads
+    if args.global_chains:
+        # one global chain set (seed 1000), this rank's contiguous shard
+        wl = workloads.make(args.workload, n_chains=args.global_chains)
+        lo, hi = shard.shard_range(args.global_chains, world, rank)
+        wl.q0, wl.p0 = wl.q0[lo:hi].copy(), wl.p0[lo:hi].copy()
+    else:
+        wl = workloads.make(args.workload, n_chains=args.chains, seed_offset=rank)
     # CPU baseline first: forked workers must not inherit an initialised GPU.
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -162,20 +172,22 @@ def main():
     wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-        wt = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(wt, op=dist.ReduceOp.MAX)
-        wall = float(wt.item())
+        wall = shard.max_over_ranks(wall)
     launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
 
     stat = st.cpu().numpy()
     nonfinite = int(((stat & capi.STATUS_NONFINITE) != 0).sum())
 
     chain_steps = wl.n_chains * leap
-    value = chain_steps * args.steps * world / wall
+    total_chains = args.global_chains or wl.n_chains * world
+    value = total_chains * leap * args.steps / wall
     npix = wl.D.size
     bpu = alg_bytes_per_step(npix, wl.K)
     achieved = bpu * chain_steps / (launch_ms * 1e-3) / 1e9
-    traffic = load_traffic(wl.name)
+    pmc = load_pmc(wl.name)
+    traffic = pmc.get("hbm_bytes_per_launch")
+    if traffic is not None and pmc.get("chain_steps_per_dispatch") not in (None, chain_steps):
+        traffic = traffic * chain_steps / pmc["chain_steps_per_dispatch"]
     out = {
         "metric": "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X",
         "value": value,
@@ -185,14 +197,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_chains else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (numpy RandomState: image seed 77, chains seed 1000+rank)",
         "config": {"workload": "%s: %dx%d image, K=%d, %d chains/GPU, %d leapfrog steps per "
                                "launch" % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K,
                                            wl.n_chains, leap),
-                   "chains_per_gpu": wl.n_chains, "image": list(wl.D.shape), "K": wl.K,
+                   "chains_per_gpu": wl.n_chains, "total_chains": total_chains,
+                   "image": list(wl.D.shape), "K": wl.K,
                    "leapfrog_steps_per_launch": leap, "parallelism": "chain-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
@@ -200,6 +213,16 @@ def main():
                      "fp64_tflops_alg": alg_flops_per_step(npix, wl.K) * chain_steps
                      / (launch_ms * 1e-3) / 1e12},
         "nonfinite_chains": nonfinite,
+    }
+    # The image is LDS-resident, so the algorithmic-HBM fraction above exceeds
+    # 1; the physically binding roof is FP64 VALU issue: executed fp64 flops per
+    # chain-step (PMC, profiles/pmc_<wl>.json) x rate / 78.6 TF/s.
+    fpc = pmc.get("fp64_flops_per_chain_step")
+    out["roofline_fp64_valu"] = None if fpc is None else {
+        "bound": "valu-fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+        "achieved": fpc * chain_steps / (launch_ms * 1e-3) / 1e12,
+        "frac": fpc * chain_steps / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+        "executed_fp64_flops_per_chain_step": fpc,
     }
     if rank == 0:
         out["cpu_baseline"] = cpu

@@ -17,6 +17,7 @@ from collections import defaultdict
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_c2"
 wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
 kernel_sub = sys.argv[3] if len(sys.argv) > 3 else "leapfrog"
+chain_steps = float(sys.argv[4]) if len(sys.argv) > 4 else 4096 * 500.
 
 vals = defaultdict(list)
 for path in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
@@ -30,6 +31,14 @@ avg = {k: sum(v) / len(v) for k, v in vals.items() if v}
 out = {"workload": wl, "kernel_filter": kernel_sub, "counters_avg_per_dispatch": avg}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     out["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
+f64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
+if all(k in avg for k in f64):
+    # executed fp64 flops (FMA = 2) over all 64 lanes, per chain-leapfrog-step
+    flops = (2 * avg[f64[0]] + avg[f64[1]] + avg[f64[2]]) * 64
+    out["chain_steps_per_dispatch"] = chain_steps
+    out["fp64_flops_per_chain_step"] = flops / chain_steps
+    out["valu_insts_per_chain_step"] = avg.get("SQ_INSTS_VALU", 0) / chain_steps
+    out["fp64_insts_per_chain_step"] = sum(avg[k] for k in f64) / chain_steps
 if "GRBM_GUI_ACTIVE" in avg:
     out["note_clock"] = "effective clock = GRBM_GUI_ACTIVE / 8 / kernel time"
 dst = os.path.join("profiles", "pmc_%s.json" % wl)
