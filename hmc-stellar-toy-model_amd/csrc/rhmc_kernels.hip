@@ -29,6 +29,7 @@
 #include "rhmc.h"
 #include "rhmc_tiled.hpp"
 #include "rhmc_wave.hpp"
+#include "rhmc_windowed.hpp"
 
 namespace rhmc {
 
@@ -187,7 +188,131 @@ __device__ __forceinline__ int64_t stage_image(double* sD, const double* __restr
   return (int64_t)blockIdx.x * waves_per_wg + (threadIdx.x / kWave);
 }
 
-// n_steps implicit generalized-leapfrog steps (sampler_RHMC.py:522-566).
+// Chain state of one wave: lane k < K owns star k (UNIFORM: K == 1 and every
+// lane mirrors star 0, so no cross-lane reduction is needed).
+struct StarState {
+  double f, x, y, pf, px, py;
+};
+
+// n_steps implicit generalized-leapfrog steps (sampler_RHMC.py:522-566) with a
+// single gradient call site: the end-of-step gradient (:551) is the next
+// step's opening one (:525).  `grad(f, x, y, gf, gx, gy)` returns dphidq.
+template <bool UNIFORM, class Grad>
+__device__ __forceinline__ void run_steps(StarState& s, bool owner, int n_steps, int rows,
+                                          int cols, const Consts& c, int& it_p, int& it_q,
+                                          unsigned& st, Grad grad) {
+  const double hdt = c.hdt;
+  for (int step = 0;; ++step) {
+    double gf, gx, gy;
+    grad(s.f, s.x, s.y, gf, gx, gy);
+    if (step > 0) {
+      // (5) closing half kick of the previous step (:551), (6) reflection (:554-564)
+      s.pf = s.pf - hdt * gf;
+      s.px = s.px - hdt * gx;
+      s.py = s.py - hdt * gy;
+      if (s.f < c.f_lim) {
+        s.pf = -s.pf;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+      if (s.x < 0.0 || s.x > (double)(rows - 1)) {
+        s.px = -s.px;
+        st |= RHMC_STATUS_REFLECT_XY;
+      }
+      if (s.y < 0.0 || s.y > (double)(cols - 1)) {
+        s.py = -s.py;
+        st |= RHMC_STATUS_REFLECT_XY;
+      }
+    }
+    if (step == n_steps) break;
+    // (1) opening half kick (:525)
+    s.pf = s.pf - hdt * gf;
+    s.px = s.px - hdt * gx;
+    s.py = s.py - hdt * gy;
+    // (2) p fixed point, flux slots only (:528-535); x/y slots change by 0
+    {
+      const double coef = dtaudq_coef(s.f, c);
+      const double rho = s.pf;
+      double dp;
+      int n = 0;
+      do {
+        const double pp = rho - hdt * ((s.pf * s.pf) * coef / 2.0);
+        const double d = (UNIFORM || owner) ? fabs(s.pf - pp) : 0.0;
+        dp = UNIFORM ? d : wave_nanmax(d);
+        s.pf = pp;
+        ++n;
+      } while (dp > c.delta && n < c.counter_max);
+      it_p += n;
+      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
+    }
+    // (3) q fixed point (:538-545): q' = sig + dt/2 (p/H(sig) + p/H(q))
+    {
+      const double sf = s.f, sx = s.x, sy = s.y;
+      const double hff0 = H_ff(sf, c), hxx0 = H_xx(sf, c);
+      const double af = s.pf / hff0, ax = s.px / hxx0, ay = s.py / hxx0;
+      double dq;
+      int n = 0;
+      do {
+        const double hff = H_ff(s.f, c), hxx = H_xx(s.f, c);
+        const double nf = sf + hdt * (af + s.pf / hff);
+        const double nx = sx + hdt * (ax + s.px / hxx);
+        const double ny = sy + hdt * (ay + s.py / hxx);
+        double d = nanmax2(nanmax2(fabs(s.f - nf), fabs(s.x - nx)), fabs(s.y - ny));
+        d = (UNIFORM || owner) ? d : 0.0;
+        dq = UNIFORM ? d : wave_nanmax(d);
+        s.f = nf;
+        s.x = nx;
+        s.y = ny;
+        ++n;
+      } while (dq > c.delta && n < c.counter_max);
+      it_q += n;
+      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
+    }
+    // (4) p -= dt/2 dtaudq(q, p) (:548)
+    s.pf = s.pf - hdt * ((s.pf * s.pf) * dtaudq_coef(s.f, c) / 2.0);
+  }
+}
+
+__device__ __forceinline__ StarState load_chain(const LeapArgs& a, int64_t chain, int K,
+                                                bool owner, int64_t& base) {
+  base = chain * 3 * (int64_t)K + 3 * (owner ? lane_id() : 0);
+  StarState s;
+  s.f = a.q[base];
+  s.x = a.q[base + 1];
+  s.y = a.q[base + 2];
+  s.pf = a.p[base];
+  s.px = a.p[base + 1];
+  s.py = a.p[base + 2];
+  return s;
+}
+
+__device__ __forceinline__ void store_chain(const LeapArgs& a, int64_t chain, int64_t base,
+                                            bool owner, const StarState& s, int it_p, int it_q,
+                                            unsigned st) {
+  if (owner) {
+    if (!(isfinite(s.f) && isfinite(s.x) && isfinite(s.y) && isfinite(s.pf) &&
+          isfinite(s.px) && isfinite(s.py)))
+      st |= RHMC_STATUS_NONFINITE;
+    a.q[base] = s.f;
+    a.q[base + 1] = s.x;
+    a.q[base + 2] = s.y;
+    a.p[base] = s.pf;
+    a.p[base + 1] = s.px;
+    a.p[base + 2] = s.py;
+  }
+  // OR the star lanes' status bits
+  unsigned all = owner ? st : 0u;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) all |= (unsigned)__shfl_xor((int)all, m, kWave);
+  if (lane_id() == 0) {
+    if (a.status) a.status[chain] = (int32_t)all;
+    if (a.fp_iters) {
+      a.fp_iters[2 * chain] = it_p;
+      a.fp_iters[2 * chain + 1] = it_q;
+    }
+  }
+}
+
+// Generic kernel: image in LDS, K <= MAXK <= 16, reference-form metric.
 template <int MAXK>
 __global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
   extern __shared__ double lds[];
@@ -197,115 +322,43 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
   double* sD = lds;
   const int64_t chain = stage_image(sD, a.D, g.npix, W);
   if (chain >= a.n_chains) return;
-  const int lane = lane_id();
   const int K = a.K;
-  const Tables tab = carve_tables(lds + g.npix + (threadIdx.x / kWave) * table_doubles(K, g.rows, g.cols), K, g);
-
-  // lane k < K owns star k
-  const bool owner = lane < K;
-  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
-  double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
-  double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
-
+  const Tables tab = carve_tables(
+      lds + g.npix + (threadIdx.x / kWave) * table_doubles(K, g.rows, g.cols), K, g);
+  const bool owner = lane_id() < K;
+  int64_t base;
+  StarState s = load_chain(a, chain, K, owner, base);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  const double hdt = c.hdt;
-  double gf, gx, gy;
-  gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
+  run_steps<MAXK == 1>(s, owner, a.n_steps, g.rows, g.cols, c, it_p, it_q, st,
+                       [&](double f, double x, double y, double& gf, double& gx, double& gy) {
+                         gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
+                       });
+  store_chain(a, chain, base, owner, s, it_p, it_q, st);
+}
 
-  for (int s = 0; s < a.n_steps; ++s) {
-    // (1) half kick with dphidq (:525)
-    pf = pf - hdt * gf;
-    px = px - hdt * gx;
-    py = py - hdt * gy;
-
-    // (2) p fixed point, flux slots only (:528-535); x/y slots change by 0
-    {
-      const double coef = dtaudq_coef(f, c);
-      const double rho = pf;
-      double dp;
-      int n = 0;
-      do {
-        const double pp = rho - hdt * ((pf * pf) * coef / 2.0);
-        double d = (MAXK == 1 || owner) ? fabs(pf - pp) : 0.0;
-        dp = (MAXK == 1) ? d : wave_nanmax(d);
-        pf = pp;
-        ++n;
-      } while (dp > c.delta && n < c.counter_max);
-      it_p += n;
-      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
-    }
-
-    // (3) q fixed point (:538-545): q' = sig + dt/2 (p/H(sig) + p/H(q))
-    {
-      const double sf = f, sx = x, sy = y;
-      const double hff0 = H_ff(sf, c), hxx0 = H_xx(sf, c);
-      const double af = pf / hff0, ax = px / hxx0, ay = py / hxx0;
-      double dq;
-      int n = 0;
-      do {
-        const double hff = H_ff(f, c), hxx = H_xx(f, c);
-        const double nf = sf + hdt * (af + pf / hff);
-        const double nx = sx + hdt * (ax + px / hxx);
-        const double ny = sy + hdt * (ay + py / hxx);
-        double d = nanmax2(nanmax2(fabs(f - nf), fabs(x - nx)), fabs(y - ny));
-        d = (MAXK == 1 || owner) ? d : 0.0;
-        dq = (MAXK == 1) ? d : wave_nanmax(d);
-        f = nf;
-        x = nx;
-        y = ny;
-        ++n;
-      } while (dq > c.delta && n < c.counter_max);
-      it_q += n;
-      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
-    }
-
-    // (4) p -= dt/2 dtaudq(q, p) (:548)
-    pf = pf - hdt * ((pf * pf) * dtaudq_coef(f, c) / 2.0);
-
-    // (5) p -= dt/2 dphidq(q) (:551); the gradient carries to the next step
-    gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
-    pf = pf - hdt * gf;
-    px = px - hdt * gx;
-    py = py - hdt * gy;
-
-    // (6) flux wall and edge reflection (:554-564)
-    if (f < c.f_lim) {
-      pf = -pf;
-      st |= RHMC_STATUS_REFLECT_F;
-    }
-    if (x < 0.0 || x > (double)(g.rows - 1)) {
-      px = -px;
-      st |= RHMC_STATUS_REFLECT_XY;
-    }
-    if (y < 0.0 || y > (double)(g.cols - 1)) {
-      py = -py;
-      st |= RHMC_STATUS_REFLECT_XY;
-    }
-  }
-
-  if (owner) {
-    if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
-          isfinite(py)))
-      st |= RHMC_STATUS_NONFINITE;
-    a.q[base] = f;
-    a.q[base + 1] = x;
-    a.q[base + 2] = y;
-    a.p[base] = pf;
-    a.p[base + 1] = px;
-    a.p[base + 2] = py;
-  }
-  // OR the star lanes' status bits (only lanes < K set reflection bits)
-  unsigned all = owner ? st : 0u;
-#pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) all |= (unsigned)__shfl_xor((int)all, m, kWave);
-  if (lane == 0) {
-    if (a.status) a.status[chain] = (int32_t)all;
-    if (a.fp_iters) {
-      a.fp_iters[2 * chain] = it_p;
-      a.fp_iters[2 * chain + 1] = it_q;
-    }
-  }
+// Windowed kernel (any square image, 1 <= K <= 64): D from global memory.
+__global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
+  extern __shared__ double lds[];
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int K = a.K;
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const LeanConsts lc = lean_consts(c);
+  const bool owner = lane_id() < K;
+  int64_t base;
+  StarState s = load_chain(a, chain, K, owner, base);
+  int it_p = 0, it_q = 0;
+  unsigned st = 0u;
+  const int rows = a.g.rows, cols = a.g.cols;
+  run_steps<false>(s, owner, a.n_steps, rows, cols, c, it_p, it_q, st,
+                   [&](double f, double x, double y, double& gf, double& gx, double& gy) {
+                     win_gradient(a.D, tab, K, f, x, y, rows, cols, c, lc, true, gf, gx, gy);
+                   });
+  store_chain(a, chain, base, owner, s, it_p, it_q, st);
 }
 
 struct GradArgs {
@@ -432,6 +485,83 @@ __global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
   if (lane == 0) a.V[chain] = v;
 }
 
+// Large-image gradient (windowed), one wave per chain.
+__global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
+  extern __shared__ double lds[];
+  const int W = blockDim.x / kWave;
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int lane = lane_id();
+  const int K = a.K;
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const LeanConsts lc = lean_consts(a.c);
+  const bool owner = lane < K;
+  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double gf, gx, gy;
+  win_gradient(a.D, tab, K, f, x, y, a.g.rows, a.g.cols, a.c, lc, a.with_metric != 0, gf, gx,
+               gy);
+  if (owner) {
+    a.grad[base] = gf;
+    a.grad[base + 1] = gx;
+    a.grad[base + 2] = gy;
+  }
+}
+
+// Large-image V and T (windowed tables, pixel-major V).
+__global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
+  extern __shared__ double lds[];
+  const Geometry& g = a.g;
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int lane = lane_id();
+  const int K = a.K;
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const LeanConsts lc = lean_consts(c);
+  const bool owner = lane < K;
+  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  if (a.T) {
+    double t1 = 0.0, t2 = 0.0;
+    if (owner) {
+      const double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+      const double hff = H_ff(f, c), hxx = H_xx(f, c);
+      t1 = pf * pf / hff + px * px / hxx + py * py / hxx;
+      t2 = log(fabs(hff)) + log(fabs(hxx)) + log(fabs(hxx));
+    }
+    t1 = wave_sum(t1);
+    t2 = wave_sum(t2);
+    if (lane == 0) a.T[chain] = (t1 + t2) / 2.0;
+  }
+  if (!a.V) return;
+  bool bad = false;
+  if (owner) {
+    if (a.f_pos && f < c.f_lim) bad = true;
+    if (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)) bad = true;
+  }
+  if (__any(bad)) {
+    if (lane == 0) a.V[chain] = INFINITY;
+    return;
+  }
+  double v = win_potential(a.D, tab, K, f, x, y, g.rows, g.cols, c, lc);
+  if (c.use_prior) v += wave_sum(owner ? c.alpha * log(f) + c.vprior : 0.0);
+  if (c.use_Vc) {
+    double s = 0.0;
+    for (int jj = 0; jj < K; ++jj) {
+      const double X = bcast(x, jj), Y = bcast(y, jj);
+      double R = sqrt((X - x) * (X - x) + (Y - y) * (Y - y));
+      if (fabs(R) < 1e-10) R = 1e32;
+      s += pow(1.0 / R, c.vc_pow);
+    }
+    v += 0.5 * c.beta * wave_sum(owner ? s : 0.0);
+  }
+  if (lane == 0) a.V[chain] = v;
+}
+
 }  // namespace rhmc
 
 // ============================================================================
@@ -466,7 +596,37 @@ struct rhmc_ctx {
 
 namespace {
 
-constexpr int kMaxKSupported = 16;
+// RHMC_KERNEL=generic / =windowed force a kernel family (the parity tests run
+// the same inputs through every path).
+bool force_generic() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  return e && std::strcmp(e, "generic") == 0;
+}
+bool force_windowed() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  return e && std::strcmp(e, "windowed") == 0;
+}
+
+constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
+constexpr int kMaxK = 64;          // windowed kernel: lanes = stars
+
+// Which kernel family serves (K, image): the LDS-image kernels need D and the
+// per-wave tables in LDS and K <= 16; everything else goes windowed.
+bool use_windowed(const rhmc_ctx* ctx, int K) {
+  if (K > kMaxKGeneric) return true;
+  const size_t need = ((size_t)ctx->rows * ctx->cols + table_doubles(K, ctx->rows, ctx->cols)) *
+                      sizeof(double);
+  return need > (size_t)ctx->max_lds || force_windowed();
+}
+
+// Windowed kernels: W waves per workgroup, LDS = W * tables.
+void pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
+  const size_t per = win_table_doubles(K) * sizeof(double);
+  int w = 4;
+  while (w > 1 && w * per > (size_t)ctx->max_lds) w >>= 1;
+  *W = w;
+  *lds = w * per;
+}
 
 Geometry make_geometry(int rows, int cols) {
   Geometry g;
@@ -533,9 +693,7 @@ int check_common(rhmc_ctx* ctx, int64_t n_chains, int32_t K) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
   if (n_chains < 0) return fail(RHMC_ERR_ARG, "n_chains < 0");
-  if (K < 1 || K > 64) return fail(RHMC_ERR_ARG, "K must be in [1, 64]");
-  if (K > kMaxKSupported)
-    return fail(RHMC_ERR_UNSUPPORTED, "K > " + std::to_string(kMaxKSupported) + " not built yet");
+  if (K < 1 || K > kMaxK) return fail(RHMC_ERR_ARG, "K must be in [1, 64]");
   if (n_chains > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "n_chains too large");
   return RHMC_OK;
 }
@@ -585,12 +743,6 @@ struct EnergyLaunch {
   }
 };
 
-// RHMC_KERNEL=generic forces the generic kernel (used by the parity tests to
-// cover both code paths on the same inputs).
-bool force_generic() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strcmp(e, "generic") == 0;
-}
 
 template <int IMG>
 int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
@@ -617,7 +769,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   if (n_chains == 0) return RHMC_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const int side = ctx->rows;
-  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
+  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() && !force_windowed() &&
       (side == 16 || side == 32 || side == 48 || side == 64)) {
     LeapArgsK1 t;
     t.q = d_q;
@@ -638,8 +790,24 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
       default: return launch_tiled<64>(ctx, t, s);
     }
   }
+  a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
+  if (use_windowed(ctx, K)) {
+    a.q = d_q;
+    a.p = d_p;
+    a.fp_iters = d_it;
+    a.status = d_st;
+    a.D = ctx->d_D;
+    a.n_chains = n_chains;
+    a.K = K;
+    a.n_steps = n_steps;
+    pick_waves_win(ctx, K, &lds, &W);
+    const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
+    hipLaunchKernelGGL(leapfrog_win_kernel, grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return RHMC_OK;
+  }
   if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
   a.q = d_q;
   a.p = d_p;
@@ -795,7 +963,11 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   if ((rc = make_consts(P, &a.c))) return rc;
   size_t lds;
   int W;
-  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
+  const bool win = use_windowed(ctx, K);
+  if (win)
+    pick_waves_win(ctx, K, &lds, &W);
+  else if ((rc = pick_waves(ctx, K, &lds, &W)))
+    return rc;
   const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
   HIP_TRY(hipSetDevice(ctx->device));
   if ((rc = ensure_scratch(ctx, 2 * sb + 256))) return rc;
@@ -810,7 +982,12 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.with_metric = kind;
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
-  if ((rc = dispatch_k<GradLaunch>(K, grid, block, lds, ctx->stream, a))) return rc;
+  if (win) {
+    hipLaunchKernelGGL(gradient_win_kernel, grid, block, lds, ctx->stream, a);
+    HIP_TRY(hipGetLastError());
+  } else if ((rc = dispatch_k<GradLaunch>(K, grid, block, lds, ctx->stream, a))) {
+    return rc;
+  }
   HIP_TRY(hipMemcpyAsync(grad, dg, sb, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RHMC_OK;
@@ -827,7 +1004,11 @@ int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const doub
   if ((rc = make_consts(P, &a.c))) return rc;
   size_t lds;
   int W;
-  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
+  const bool win = use_windowed(ctx, K);
+  if (win)
+    pick_waves_win(ctx, K, &lds, &W);
+  else if ((rc = pick_waves(ctx, K, &lds, &W)))
+    return rc;
   const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
   const size_t eb = (size_t)n_chains * sizeof(double);
   HIP_TRY(hipSetDevice(ctx->device));
@@ -849,7 +1030,12 @@ int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const doub
   a.f_pos = f_pos != 0;
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
-  if ((rc = dispatch_k<EnergyLaunch>(K, grid, block, lds, ctx->stream, a))) return rc;
+  if (win) {
+    hipLaunchKernelGGL(energy_win_kernel, grid, block, lds, ctx->stream, a);
+    HIP_TRY(hipGetLastError());
+  } else if ((rc = dispatch_k<EnergyLaunch>(K, grid, block, lds, ctx->stream, a))) {
+    return rc;
+  }
   if (V) HIP_TRY(hipMemcpyAsync(V, dV, eb, hipMemcpyDeviceToHost, ctx->stream));
   if (T) HIP_TRY(hipMemcpyAsync(T, dT, eb, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));

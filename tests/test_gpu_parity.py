@@ -21,8 +21,21 @@ def _ctx(capi, z):
     return capi.Context(z["D"])
 
 
+@pytest.fixture(params=["auto", "generic", "windowed"])
+def kernel_path(request, monkeypatch):
+    """Run a test on the automatically chosen kernel, then again forced onto
+    the generic LDS-image kernel and onto the windowed large-image kernel."""
+    if request.param != "auto":
+        monkeypatch.setenv("RHMC_KERNEL", request.param)
+    else:
+        monkeypatch.delenv("RHMC_KERNEL", raising=False)
+    return request.param
+
+
+
+
 @pytest.mark.parametrize("name", ["k1", "k1gff2", "k10", "vc5"])
-def test_gradient_and_energy(gpu_lib, name):
+def test_gradient_and_energy(gpu_lib, kernel_path, name):
     capi = gpu_lib
     z = load_golden("functions")
     par = R.params_from_npz(z, name + "/par_")
@@ -71,7 +84,8 @@ def test_single_steps(gpu_lib):
 TRAJ = [("traj_c1", 1e-9, 1e-8, None), ("traj_c2", 1e-9, 1e-8, None),
         ("traj_gff2", 1e-9, 1e-8, None), ("traj_c3", 1e-9, 1e-8, 100),
         ("traj_prior", 1e-9, 1e-8, None), ("traj_vc", 1e-9, 1e-8, None),
-        ("traj_edge", 1e-9, 1e-8, None), ("traj_cmax", 1e-9, 1e-8, None)]
+        ("traj_edge", 1e-9, 1e-8, None), ("traj_cmax", 1e-9, 1e-8, None),
+        ("traj_c5", 1e-9, 1e-8, None)]
 
 
 @pytest.mark.parametrize("name,qtol,ptol,horizon", TRAJ)
@@ -92,17 +106,6 @@ def test_trajectory_stepwise(gpu_lib, name, qtol, ptol, horizon):
         np.testing.assert_array_equal(it[:, 1], z["n_q"][:, s], err_msg="q-iters step %d" % s)
         assert_state_close(q, Q[:, s + 1], 1e-11, "%s q step %d" % (name, s))
         assert_state_close(p, Pm[:, s + 1], 1e-10, "%s p step %d" % (name, s))
-
-
-@pytest.fixture(params=["auto", "generic"])
-def kernel_path(request, monkeypatch):
-    """Run a test on the specialised single-star kernel (auto) and again on
-    the generic kernel (RHMC_KERNEL=generic)."""
-    if request.param == "generic":
-        monkeypatch.setenv("RHMC_KERNEL", "generic")
-    else:
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
-    return request.param
 
 
 @pytest.mark.parametrize("name,qtol,ptol,horizon", TRAJ)
@@ -161,6 +164,25 @@ def test_oracle_matches_gpu_random_chains(gpu_lib, kernel_path):
         assert_state_close(pg[c], po, 1e-8, "p")
 
 
+def test_c5_gradient_energy_vs_oracle(gpu_lib):
+    """256x256, K=64 with prior (windowed kernel) against the full-image oracle."""
+    capi = gpu_lib
+    z = load_golden("traj_c5")
+    par = R.params_from_npz(z)
+    ctx = _ctx(capi, z)
+    P = capi_params(capi, par)
+    m = R.RefModel(z["D"], par)
+    q, p = z["Q"][0, :2], z["P"][0, :2]
+    g = ctx.gradient(P, q, kind=1)
+    for c in range(2):
+        want = m.dphidq(q[c])
+        assert np.abs(g[c] - want).max() / (np.abs(want).max() + 1) < 1e-10
+    V, T = ctx.energy(P, q, p, f_pos=True)
+    for c in range(2):
+        np.testing.assert_allclose(V[c], m.V(q[c], f_pos=True), rtol=1e-12)
+        np.testing.assert_allclose(T[c], m.T(p[c], m.H(q[c])), rtol=1e-12)
+
+
 def test_errors(gpu_lib):
     capi = gpu_lib
     z = load_golden("traj_c1")
@@ -171,6 +193,8 @@ def test_errors(gpu_lib):
     P = capi_params(capi, par)
     with pytest.raises(capi.RhmcError):
         ctx.leapfrog(P, np.zeros((2, 3 * 65)), np.zeros((2, 3 * 65)), 1)   # K > 64
+    with pytest.raises(capi.RhmcError):
+        ctx.gradient(P, np.zeros((2, 0)))                                # K = 0
     bad = capi_params(capi, par)
     bad.reserved = 1
     with pytest.raises(capi.RhmcError):
