@@ -28,6 +28,7 @@
 
 #include "rhmc.h"
 #include "rhmc_tiled.hpp"
+#include "rhmc_tiledk.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 
@@ -334,6 +335,36 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
                        [&](double f, double x, double y, double& gf, double& gx, double& gy) {
                          gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
                        });
+  store_chain(a, chain, base, owner, s, it_p, it_q, st);
+}
+
+// Multi-star tiled kernel (2 <= K <= KMAX <= 16, IMG x IMG image, IMG in {32, 48}).
+template <int IMG, int KMAX>
+__global__ void __launch_bounds__(256) leapfrog_tiledk_kernel(LeapArgs a) {
+  using TK = TiledK<IMG, KMAX>;
+  extern __shared__ double lds[];
+  const int W = blockDim.x / kWave;
+  for (int e = threadIdx.x; e < TK::NPIX; e += blockDim.x) {
+    const int r = e / IMG, cc = e - (e / IMG) * IMG;
+    lds[Tiled<IMG>::tiled_index(r, cc)] = a.D[e];
+  }
+  __syncthreads();
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int K = a.K;
+  double* tab = lds + TK::NPIX + (threadIdx.x / kWave) * TK::TAB;
+  const double* sDl = lds + lane_id();
+  const Consts& c = a.c;
+  const LeanConsts lc = lean_consts(c);
+  const bool owner = lane_id() < K;
+  int64_t base;
+  StarState s = load_chain(a, chain, K, owner, base);
+  int it_p = 0, it_q = 0;
+  unsigned st = 0u;
+  run_steps<false>(s, owner, a.n_steps, IMG, IMG, c, it_p, it_q, st,
+                   [&](double f, double x, double y, double& gf, double& gx, double& gy) {
+                     TK::gradient(sDl, tab, K, f, x, y, c, lc, gf, gx, gy);
+                   });
   store_chain(a, chain, base, owner, s, it_p, it_q, st);
 }
 
@@ -758,6 +789,28 @@ int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
+template <int IMG, int KMAX>
+int launch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
+  using TK = TiledK<IMG, KMAX>;
+  int W = 4;
+  while (W > 1 && TK::lds_doubles(W) * sizeof(double) > (size_t)ctx->max_lds) W >>= 1;
+  const size_t lds = TK::lds_doubles(W) * sizeof(double);
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "tiledk LDS");
+  const dim3 grid((unsigned)((a.n_chains + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_tiledk_kernel<IMG, KMAX>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
+template <int IMG>
+int dispatch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
+  if (a.K <= 2) return launch_tiledk<IMG, 2>(ctx, a, s);
+  if (a.K <= 4) return launch_tiledk<IMG, 4>(ctx, a, s);
+  if (a.K <= 8) return launch_tiledk<IMG, 8>(ctx, a, s);
+  if (a.K <= 10) return launch_tiledk<IMG, 10>(ctx, a, s);
+  return launch_tiledk<IMG, 16>(ctx, a, s);
+}
+
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s) {
@@ -808,7 +861,6 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     HIP_TRY(hipGetLastError());
     return RHMC_OK;
   }
-  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
   a.q = d_q;
   a.p = d_p;
   a.fp_iters = d_it;
@@ -817,8 +869,9 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   a.n_chains = n_chains;
   a.K = K;
   a.n_steps = n_steps;
-  a.g = make_geometry(ctx->rows, ctx->cols);
-  HIP_TRY(hipSetDevice(ctx->device));
+  if (K >= 2 && K <= kMaxKGeneric && !force_generic() && (side == 32 || side == 48))
+    return side == 32 ? dispatch_tiledk<32>(ctx, a, s) : dispatch_tiledk<48>(ctx, a, s);
+  if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   return dispatch_k<LeapLaunch>(K, grid, block, lds, s, a);
 }
