@@ -177,6 +177,12 @@ def main():
 
     stat = st.cpu().numpy()
     nonfinite = int(((stat & capi.STATUS_NONFINITE) != 0).sum())
+    iters = it.cpu().numpy()            # last launch: sums over its `leap` steps
+    fp_stats = {"p_loop_mean": float(iters[:, 0].mean() / max(leap, 1)),
+                "q_loop_mean": float(iters[:, 1].mean() / max(leap, 1)),
+                "p_loop_cap_chains": int(((stat & capi.STATUS_PLOOP_CAP) != 0).sum()),
+                "q_loop_cap_chains": int(((stat & capi.STATUS_QLOOP_CAP) != 0).sum()),
+                "flux_wall_chains": int(((stat & capi.STATUS_REFLECT_F) != 0).sum())}
 
     chain_steps = wl.n_chains * leap
     total_chains = args.global_chains or wl.n_chains * world
@@ -213,6 +219,7 @@ def main():
                      "fp64_tflops_alg": alg_flops_per_step(npix, wl.K) * chain_steps
                      / (launch_ms * 1e-3) / 1e12},
         "nonfinite_chains": nonfinite,
+        "fixed_point_iters_per_step": fp_stats,
     }
     # The image is LDS-resident, so the algorithmic-HBM fraction above exceeds
     # 1; the physically binding roof is FP64 VALU issue: executed fp64 flops per
