@@ -27,6 +27,7 @@
 #include <string>
 
 #include "rhmc.h"
+#include "rhmc_mh.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiledk.hpp"
 #include "rhmc_wave.hpp"
@@ -622,6 +623,8 @@ struct rhmc_ctx {
   // scratch for the host-pointer entry points
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
+  void* mh_scratch = nullptr;      // MH driver work arrays (q', p, V, V', E0)
+  size_t mh_scratch_bytes = 0;
   int max_lds = 0;
 };
 
@@ -789,6 +792,37 @@ int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
+// V (and optionally T) of n chains on device buffers, async on `s`.
+int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const double* d_p,
+                  double* d_V, double* d_T, int64_t n, int K, int f_pos, hipStream_t s) {
+  EnergyArgs a;
+  a.c = c;
+  size_t lds;
+  int W;
+  int rc;
+  const bool win = use_windowed(ctx, K);
+  if (win)
+    pick_waves_win(ctx, K, &lds, &W);
+  else if ((rc = pick_waves(ctx, K, &lds, &W)))
+    return rc;
+  a.q = d_q;
+  a.p = d_p;
+  a.V = d_V;
+  a.T = d_T;
+  a.D = ctx->d_D;
+  a.n_chains = n;
+  a.K = K;
+  a.f_pos = f_pos != 0;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+  if (win) {
+    hipLaunchKernelGGL(energy_win_kernel, grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return RHMC_OK;
+  }
+  return dispatch_k<EnergyLaunch>(K, grid, block, lds, s, a);
+}
+
 template <int IMG, int KMAX>
 int launch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
   using TK = TiledK<IMG, KMAX>;
@@ -876,6 +910,66 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   return dispatch_k<LeapLaunch>(K, grid, block, lds, s, a);
 }
 
+int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                    int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
+                    hipStream_t s);
+
+// The MH outer loop on device buffers (sampler_RHMC.py:1018-1083): per
+// iteration begin -> n_steps fused leapfrog -> V(q') -> accept, all queued on
+// `s` with no host synchronisation.  `rec` holds device pointers (nullable).
+int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t K,
+           int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z, const double* d_u,
+           uint64_t seed, const rhmc_mh_record* rec, hipStream_t s) {
+  Consts c;
+  int rc = make_consts(P, &c);
+  if (rc) return rc;
+  if (n_iter < 0 || n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter/n_steps < 0");
+  if (n == 0 || n_iter == 0) return RHMC_OK;
+  const size_t sb = (size_t)n * 3 * K * sizeof(double), eb = (size_t)n * sizeof(double);
+  const size_t need = 2 * sb + 3 * eb + 256;
+  if (need > ctx->mh_scratch_bytes) {
+    if (ctx->mh_scratch) HIP_TRY(hipFree(ctx->mh_scratch));
+    ctx->mh_scratch = nullptr;
+    ctx->mh_scratch_bytes = 0;
+    if (hipMalloc(&ctx->mh_scratch, need) != hipSuccess)
+      return fail(RHMC_ERR_NOMEM, "hipMalloc MH scratch failed");
+    ctx->mh_scratch_bytes = need;
+  }
+  char* b = (char*)ctx->mh_scratch;
+  MhArgs m;
+  m.q = d_q;
+  m.q_prop = (double*)b;
+  m.p = (double*)(b + sb);
+  m.V_cur = (double*)(b + 2 * sb);
+  m.V_prop = (double*)(b + 2 * sb + eb);
+  m.E0 = (double*)(b + 2 * sb + 2 * eb);
+  m.z = d_z;
+  m.u = d_u;
+  m.q_chain = rec ? rec->q_chain : nullptr;
+  m.E_chain = rec ? rec->E_chain : nullptr;
+  m.V_chain = rec ? rec->V_chain : nullptr;
+  m.T_chain = rec ? rec->T_chain : nullptr;
+  m.accept = rec ? rec->accept : nullptr;
+  m.n = n;
+  m.K = K;
+  m.seed = seed;
+  m.c = c;
+  if ((rc = launch_energy(ctx, c, d_q, nullptr, m.V_cur, nullptr, n, K, f_pos, s))) return rc;
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  for (int it = 0; it < n_iter; ++it) {
+    m.iter = it;
+    hipLaunchKernelGGL(mh_begin_kernel, grid, block, 0, s, m);
+    HIP_TRY(hipGetLastError());
+    if ((rc = launch_leapfrog(ctx, P, m.q_prop, m.p, n, K, n_steps, nullptr, nullptr, s)))
+      return rc;
+    if ((rc = launch_energy(ctx, c, m.q_prop, nullptr, m.V_prop, nullptr, n, K, f_pos, s)))
+      return rc;
+    hipLaunchKernelGGL(mh_end_kernel, grid, block, 0, s, m);
+    HIP_TRY(hipGetLastError());
+  }
+  return RHMC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -956,6 +1050,7 @@ void rhmc_ctx_destroy(rhmc_ctx* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_D) (void)hipFree(ctx->d_D);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->mh_scratch) (void)hipFree(ctx->mh_scratch);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -1053,15 +1148,8 @@ int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const doub
   if (n_chains == 0) return RHMC_OK;
   if (!q) return fail(RHMC_ERR_ARG, "q is NULL");
   if (T && !p) return fail(RHMC_ERR_ARG, "T requested but p is NULL");
-  EnergyArgs a;
-  if ((rc = make_consts(P, &a.c))) return rc;
-  size_t lds;
-  int W;
-  const bool win = use_windowed(ctx, K);
-  if (win)
-    pick_waves_win(ctx, K, &lds, &W);
-  else if ((rc = pick_waves(ctx, K, &lds, &W)))
-    return rc;
+  Consts c;
+  if ((rc = make_consts(P, &c))) return rc;
   const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
   const size_t eb = (size_t)n_chains * sizeof(double);
   HIP_TRY(hipSetDevice(ctx->device));
@@ -1073,24 +1161,74 @@ int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const doub
   double* dT = (double*)(base + 2 * sb + eb);
   HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
   if (T) HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
-  a.q = dq;
-  a.p = T ? dp : nullptr;
-  a.V = V ? dV : nullptr;
-  a.T = T ? dT : nullptr;
-  a.D = ctx->d_D;
-  a.n_chains = n_chains;
-  a.K = K;
-  a.f_pos = f_pos != 0;
-  a.g = make_geometry(ctx->rows, ctx->cols);
-  const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
-  if (win) {
-    hipLaunchKernelGGL(energy_win_kernel, grid, block, lds, ctx->stream, a);
-    HIP_TRY(hipGetLastError());
-  } else if ((rc = dispatch_k<EnergyLaunch>(K, grid, block, lds, ctx->stream, a))) {
+  if ((rc = launch_energy(ctx, c, dq, T ? dp : nullptr, V ? dV : nullptr, T ? dT : nullptr,
+                          n_chains, K, f_pos, ctx->stream)))
     return rc;
-  }
   if (V) HIP_TRY(hipMemcpyAsync(V, dV, eb, hipMemcpyDeviceToHost, ctx->stream));
   if (T) HIP_TRY(hipMemcpyAsync(T, dT, eb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
+                   int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
+                   const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains > 0 && !d_q) return fail(RHMC_ERR_ARG, "q is NULL");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return run_mh(ctx, P, d_q, n_chains, K, n_iter, n_steps, f_pos, d_z, d_u, seed, rec, s);
+}
+
+int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, int32_t K,
+            int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* z, const double* u,
+            uint64_t seed, const rhmc_mh_record* rec) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0 || n_iter == 0) return RHMC_OK;
+  if (!q) return fail(RHMC_ERR_ARG, "q is NULL");
+  if (n_iter < 0) return fail(RHMC_ERR_ARG, "n_iter < 0");
+  const size_t d = (size_t)3 * K;
+  const size_t sb = (size_t)n_chains * d * sizeof(double);
+  const size_t zb = z ? (size_t)n_iter * sb : 0;
+  const size_t ub = u ? (size_t)n_iter * n_chains * sizeof(double) : 0;
+  const size_t qcb = (rec && rec->q_chain) ? (size_t)n_iter * sb : 0;
+  const size_t eb = (size_t)n_iter * n_chains * sizeof(double);
+  const size_t ab = (size_t)n_iter * n_chains * sizeof(int32_t);
+  size_t off[8], tot = 0;
+  const size_t parts[8] = {sb, zb, ub, qcb, (rec && rec->E_chain) ? eb : 0,
+                           (rec && rec->V_chain) ? eb : 0, (rec && rec->T_chain) ? eb : 0,
+                           (rec && rec->accept) ? ab : 0};
+  for (int i = 0; i < 8; ++i) {
+    off[i] = tot;
+    tot += (parts[i] + 255) & ~(size_t)255;
+  }
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, tot + 256))) return rc;
+  char* b = (char*)ctx->scratch;
+  double* dq = (double*)(b + off[0]);
+  const double* dz = z ? (const double*)(b + off[1]) : nullptr;
+  const double* du = u ? (const double*)(b + off[2]) : nullptr;
+  rhmc_mh_record drec{qcb ? (double*)(b + off[3]) : nullptr,
+                      parts[4] ? (double*)(b + off[4]) : nullptr,
+                      parts[5] ? (double*)(b + off[5]) : nullptr,
+                      parts[6] ? (double*)(b + off[6]) : nullptr,
+                      parts[7] ? (int32_t*)(b + off[7]) : nullptr};
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  if (z) HIP_TRY(hipMemcpyAsync((void*)dz, z, zb, hipMemcpyHostToDevice, ctx->stream));
+  if (u) HIP_TRY(hipMemcpyAsync((void*)du, u, ub, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = run_mh(ctx, P, dq, n_chains, K, n_iter, n_steps, f_pos, dz, du, seed, &drec,
+                   ctx->stream)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
+  if (rec) {
+    if (rec->q_chain) HIP_TRY(hipMemcpyAsync(rec->q_chain, drec.q_chain, qcb, hipMemcpyDeviceToHost, ctx->stream));
+    if (rec->E_chain) HIP_TRY(hipMemcpyAsync(rec->E_chain, drec.E_chain, eb, hipMemcpyDeviceToHost, ctx->stream));
+    if (rec->V_chain) HIP_TRY(hipMemcpyAsync(rec->V_chain, drec.V_chain, eb, hipMemcpyDeviceToHost, ctx->stream));
+    if (rec->T_chain) HIP_TRY(hipMemcpyAsync(rec->T_chain, drec.T_chain, eb, hipMemcpyDeviceToHost, ctx->stream));
+    if (rec->accept) HIP_TRY(hipMemcpyAsync(rec->accept, drec.accept, ab, hipMemcpyDeviceToHost, ctx->stream));
+  }
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RHMC_OK;
 }

@@ -30,7 +30,8 @@ STATUS_REFLECT_XY = 16
 EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
            "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
-           "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy")
+           "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
+           "rhmc_mh_device")
 
 
 class RhmcParams(ctypes.Structure):
@@ -47,6 +48,13 @@ class RhmcParams(ctypes.Structure):
         ("counter_max", ctypes.c_int32), ("use_prior", ctypes.c_int32),
         ("use_Vc", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
+
+
+class MhRecord(ctypes.Structure):
+    """Mirror of `rhmc_mh_record` (include/rhmc.h); all fields nullable."""
+    _fields_ = [("q_chain", ctypes.c_void_p), ("E_chain", ctypes.c_void_p),
+                ("V_chain", ctypes.c_void_p), ("T_chain", ctypes.c_void_p),
+                ("accept", ctypes.c_void_p)]
 
 
 class RhmcError(RuntimeError):
@@ -84,6 +92,12 @@ def _load():
                                          ctypes.c_int32, ctypes.c_int32]),
         "rhmc_energy": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_dp,
                                        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_mh": (ctypes.c_int, [vp, P(RhmcParams), c_dp, ctypes.c_int64, ctypes.c_int32,
+                                   ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp,
+                                   ctypes.c_uint64, P(MhRecord)]),
+        "rhmc_mh_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
+                                          ctypes.c_uint64, P(MhRecord), vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -246,3 +260,43 @@ class Context:
         if single:
             return V[0], (None if T is None else T[0])
         return V, T
+
+    def mh(self, params, q, n_iter, n_steps, f_pos=True, z=None, u=None, seed=0, record=True):
+        """n_iter MH iterations (run_RHMC move-0 branch) of n_steps leapfrog steps
+        on every chain of q [n_chains, 3K].  z [n_iter, n_chains, 3K] / u
+        [n_iter, n_chains]: host randoms (None = Philox on device).  Returns a
+        dict with the final q and, when record, q_chain/E_chain/V_chain/T_chain
+        [n_iter, n_chains(, 3K)] and accept [n_iter, n_chains]."""
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        single = q2.ndim == 1
+        q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
+        n, d = q2.shape
+        zz = None if z is None else _f64(z, "z").reshape(n_iter, n, d)
+        uu = None if u is None else _f64(u, "u").reshape(n_iter, n)
+        out = {}
+        rec = None
+        if record:
+            out["q_chain"] = np.empty((n_iter, n, d))
+            for k in ("E_chain", "V_chain", "T_chain"):
+                out[k] = np.empty((n_iter, n))
+            out["accept"] = np.empty((n_iter, n), np.int32)
+            rec = MhRecord(out["q_chain"].ctypes.data, out["E_chain"].ctypes.data,
+                           out["V_chain"].ctypes.data, out["T_chain"].ctypes.data,
+                           out["accept"].ctypes.data)
+        _check(_lib.rhmc_mh(self._h, ctypes.byref(params), _dptr(q2), n, d // 3, int(n_iter),
+                            int(n_steps), int(bool(f_pos)),
+                            None if zz is None else _dptr(zz), None if uu is None else _dptr(uu),
+                            ctypes.c_uint64(int(seed)), None if rec is None else ctypes.byref(rec)))
+        out["q"] = q2[0] if single else q2
+        return out
+
+    def mh_device(self, params, q_ptr, n_chains, K, n_iter, n_steps, f_pos=True, z_ptr=None,
+                  u_ptr=None, seed=0, record=None, stream=None):
+        """Device-pointer variant (asynchronous on `stream`); record: MhRecord of
+        device pointers or None."""
+        _check(_lib.rhmc_mh_device(self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr),
+                                   int(n_chains), int(K), int(n_iter), int(n_steps),
+                                   int(bool(f_pos)), ctypes.c_void_p(z_ptr or 0),
+                                   ctypes.c_void_p(u_ptr or 0), ctypes.c_uint64(int(seed)),
+                                   None if record is None else ctypes.byref(record),
+                                   ctypes.c_void_p(stream or 0)))

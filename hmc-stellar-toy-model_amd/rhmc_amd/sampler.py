@@ -431,6 +431,50 @@ class multi_gym(base_class):
         print("Finished. Final report.")                  # :1195-1196
         self.R_accept_report(idx_iter=-1, running=False)
 
+    def run_RHMC_batched(self, q_model_0, f_pos=True, delta=1e-6, Niter=100, Nsteps=100,
+                         dt=1e-1, counter_max=1000, rng="numpy", seeds=None, seed=0):
+        """Many independent chains of run_RHMC's move-0 loop, entirely on the GPU
+        (rhmc_mh): Niter+1 MH iterations of Nsteps fused leapfrog steps.
+
+        q_model_0: [n_chains, K, 3] (mag, x, y) or [K, 3] (one chain).
+        rng="numpy": host randoms in the reference's per-iteration order
+            (randn(d), the move-type uniform, the accept uniform); from the
+            global np.random stream (iteration-major, chain-minor) or, with
+            seeds=[...], from one RandomState per chain — then chain c equals
+            run_RHMC after np.random.seed(seeds[c]).
+        rng="device": Philox-4x32-10 on the device, keyed by `seed`.
+        Sets q_chain/p-less E/V/T_chain [Niter+1, n_chains(, 3K)], A_chain
+        [Niter+1, n_chains] and returns the final q [n_chains, 3K]."""
+        q0 = np.array(q_model_0, dtype=np.float64)
+        if q0.ndim == 2:
+            q0 = q0[None]
+        n, K = q0.shape[0], q0.shape[1]
+        q0 = q0.copy()
+        q0[:, :, 0] = self.mag2flux_converter(q0[:, :, 0])
+        q0 = q0.reshape(n, 3 * K)
+        self.dt, self.Niter, self.Nsteps, self.Nobjs, self.d = dt, Niter, Nsteps, K, 3 * K
+        n_iter = Niter + 1
+        z = u = None
+        if rng == "numpy":
+            z = np.empty((n_iter, n, 3 * K))
+            u = np.empty((n_iter, n))
+            streams = [np.random.RandomState(s) for s in seeds] if seeds is not None else None
+            for l in range(n_iter):
+                for c in range(n):
+                    r = streams[c] if streams is not None else np.random
+                    z[l, c] = r.randn(3 * K)          # u_sample (:1022)
+                    r.random_sample()                 # np.random.choice move type (:1046)
+                    u[l, c] = r.random_sample()       # np.random.random(1) (:1075)
+        elif rng != "device":
+            raise ValueError("rng must be 'numpy' or 'device'")
+        self._check_geometry()
+        out = self._context().mh(self._params(delta, counter_max, for_energy=True), q0, n_iter,
+                                 Nsteps, f_pos=f_pos, z=z, u=u, seed=seed, record=True)
+        self.q_chain, self.E_chain = out["q_chain"], out["E_chain"]
+        self.V_chain, self.T_chain = out["V_chain"], out["T_chain"]
+        self.A_chain = out["accept"].astype(bool)
+        return out["q"]
+
     def R_accept_report(self, idx_iter, cumulative=True, running=True, run_window=10):
         """sampler_RHMC.py:1447-1473"""
         def rep(A, M):

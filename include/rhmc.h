@@ -20,6 +20,11 @@
  *       base_class.V (sampler_RHMC.py:294-351) and base_class.T (:353-363)
  *       at H(q) (:229-258) — the trajectory-endpoint energies of the MH test
  *       (:1021-1026, :1070-1071).
+ *   rhmc_mh / rhmc_mh_device
+ *       multi_gym.run_RHMC, move-0 ("within") branch (sampler_RHMC.py:1018-1083):
+ *       momentum draw p = z*sqrt(H(q)) (:1021-1022), E0 = V + T (:1025-1027),
+ *       Nsteps leapfrog steps (:1053-1054), E1, accept if dE < 0 or
+ *       ln u < -dE (:1072-1083) — n_iter iterations, all on the device.
  *   rhmc_ctx_create / rhmc_ctx_set_image
  *       the instance attribute base_class.D set by gen_mock_data
  *       (sampler_RHMC.py:77-99); uploaded once per context.
@@ -133,6 +138,34 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
 int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
                 const double* p, double* V, double* T, int64_t n_chains,
                 int32_t K, int32_t f_pos);
+
+/* Per-iteration records of rhmc_mh (all nullable; host pointers for rhmc_mh,
+ * device pointers for rhmc_mh_device).  Row l holds the state at the START
+ * of iteration l, like the reference's q_chain / E_chain / V_chain / T_chain
+ * (:1038-1042); accept[l] is A_chain[l] (:1077). */
+typedef struct rhmc_mh_record {
+  double* q_chain;   /* [n_iter][n_chains][3K] */
+  double* E_chain;   /* [n_iter][n_chains] */
+  double* V_chain;   /* [n_iter][n_chains] */
+  double* T_chain;   /* [n_iter][n_chains] */
+  int32_t* accept;   /* [n_iter][n_chains] */
+} rhmc_mh_record;
+
+/*
+ * n_iter MH iterations of n_steps leapfrog steps each on every chain; q
+ * [n_chains][3K] is updated in place to the last accepted state.  Randoms:
+ * z [n_iter][n_chains][3K] standard normals and u [n_iter][n_chains] uniforms
+ * in (0,1] — pass the reference's own NumPy draws for bit-level parity of the
+ * accept sequence; NULL draws them on the device (Philox-4x32-10, `seed`,
+ * counter = (index, iteration, chain)).  P->V_prior_const must be set when
+ * use_prior.
+ */
+int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, int32_t K,
+            int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* z, const double* u,
+            uint64_t seed, const rhmc_mh_record* rec);
+int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
+                   int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
+                   const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream);
 
 #ifdef __cplusplus
 }

@@ -84,3 +84,62 @@ def test_RHMC_single_step_matches_reference(gpu_lib):
         q1, p1 = g.RHMC_single_step(z["q0"][i], z["p0"][i])
         assert_state_close(q1, z["q1"][i], 1e-11, "q")
         assert_state_close(p1, z["p1"][i], 1e-10, "p")
+
+
+@pytest.mark.parametrize("name", ["mh1", "mh3"])
+def test_run_RHMC_batched_one_chain_equals_reference(gpu_lib, name):
+    """The fully on-device MH loop (rhmc_mh) fed the reference's own NumPy
+    draws reproduces the reference chain (accept sequence exactly)."""
+    z = load_golden("mh")
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    np.random.seed(int(z[name + "/seed"]))
+    niter = int(z[name + "/niter"])
+    g.run_RHMC_batched(z[name + "/q_model"].copy(), f_pos=True, Niter=niter,
+                       Nsteps=int(z[name + "/nsteps"]), dt=float(z[name + "/dt"]))
+    np.testing.assert_array_equal(g.A_chain[:, 0].astype(np.int32), z[name + "/A_chain"])
+    K3 = g.q_chain.shape[2]
+    assert_state_close(g.q_chain[:, 0], z[name + "/q_chain"][:, :K3], 1e-9, "q_chain")
+    np.testing.assert_allclose(g.E_chain[:, 0], z[name + "/E_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.V_chain[:, 0], z[name + "/V_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.T_chain[:, 0], z[name + "/T_chain"], rtol=1e-10, atol=1e-10)
+
+
+def test_run_RHMC_batched_many_chains_equal_single_runs(gpu_lib):
+    """Chains with their own RandomState seeds equal one run_RHMC per seed."""
+    z = load_golden("mh")
+    par = R.params_from_npz(z, "mh3/par_")
+    seeds = [123, 7, 99]
+    g = _gym(par)
+    g.D = z["mh3/D"]
+    qm = z["mh3/q_model"]
+    g.run_RHMC_batched(np.stack([qm] * 3), f_pos=True, Niter=10, Nsteps=10, dt=0.05,
+                       seeds=seeds)
+    Ab, qb = g.A_chain.copy(), g.q_chain.copy()
+    for c, s in enumerate(seeds):
+        h = _gym(par)
+        h.D = z["mh3/D"]
+        np.random.seed(s)
+        h.run_RHMC(qm.copy(), f_pos=True, Niter=10, Nsteps=10, dt=0.05, N_max=3)
+        np.testing.assert_array_equal(Ab[:, c], h.A_chain)
+        assert_state_close(qb[:, c], h.q_chain, 1e-12, "chain %d" % c)
+
+
+def test_mh_device_rng_deterministic_and_sane(gpu_lib):
+    z = load_golden("mh")
+    par = R.params_from_npz(z, "mh1/par_")
+    g = _gym(par)
+    g.D = z["mh1/D"]
+    qm = np.stack([z["mh1/q_model"]] * 64)
+    q1 = g.run_RHMC_batched(qm, Niter=30, Nsteps=10, dt=0.1, rng="device", seed=42)
+    A1, E1 = g.A_chain.copy(), g.E_chain.copy()
+    q2 = g.run_RHMC_batched(qm, Niter=30, Nsteps=10, dt=0.1, rng="device", seed=42)
+    assert np.array_equal(q1, q2) and np.array_equal(A1, g.A_chain)
+    q3 = g.run_RHMC_batched(qm, Niter=30, Nsteps=10, dt=0.1, rng="device", seed=43)
+    assert not np.array_equal(q1, q3)
+    assert np.isfinite(E1).all() and np.isfinite(q1).all()
+    rate = A1.mean()
+    assert 0.3 < rate <= 1.0, rate          # small-dt RHMC: high acceptance
+    # chains decorrelate: not all identical after 30 iterations
+    assert np.unique(q1[:, 1]).size > 32
