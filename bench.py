@@ -111,6 +111,10 @@ def main():
                     help="total chains split over the ranks (strong scaling, e.g. C4 = 2^20)")
     ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", choices=("leapfrog", "mh"), default="leapfrog",
+                    help="mh: whole MH iterations on device (momentum draw, V+T, accept; "
+                         "Philox RNG); one bench step = --mh-iter iterations of --leap steps")
+    ap.add_argument("--mh-iter", type=int, default=10)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -150,9 +154,16 @@ def main():
     # timing events are recorded on it.
     stream = torch.cuda.Stream(dev)
 
-    def launch():
-        ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
-                            it.data_ptr(), st.data_ptr(), stream.cuda_stream)
+    if args.mode == "mh":
+        leap = args.leap or 10
+
+        def launch():
+            ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap, f_pos=True,
+                          seed=1234 + rank, stream=stream.cuda_stream)
+    else:
+        def launch():
+            ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
+                                it.data_ptr(), st.data_ptr(), stream.cuda_stream)
 
     for _ in range(args.warmup):
         launch()
@@ -184,9 +195,10 @@ def main():
                 "q_loop_cap_chains": int(((stat & capi.STATUS_QLOOP_CAP) != 0).sum()),
                 "flux_wall_chains": int(((stat & capi.STATUS_REFLECT_F) != 0).sum())}
 
-    chain_steps = wl.n_chains * leap
+    steps_per_launch = leap * (args.mh_iter if args.mode == "mh" else 1)
+    chain_steps = wl.n_chains * steps_per_launch
     total_chains = args.global_chains or wl.n_chains * world
-    value = total_chains * leap * args.steps / wall
+    value = total_chains * steps_per_launch * args.steps / wall
     npix = wl.D.size
     bpu = alg_bytes_per_step(npix, wl.K)
     achieved = bpu * chain_steps / (launch_ms * 1e-3) / 1e9
@@ -212,7 +224,8 @@ def main():
                                            wl.n_chains, leap),
                    "chains_per_gpu": wl.n_chains, "total_chains": total_chains,
                    "image": list(wl.D.shape), "K": wl.K,
-                   "leapfrog_steps_per_launch": leap, "parallelism": "chain-sharded x%d" % world},
+                   "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
+                   "parallelism": "chain-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "alg_bytes_per_chain_step": bpu, "kernel_ms": launch_ms,

@@ -84,6 +84,12 @@ def make(name, n_chains=None, seed_offset=0):
         n, K = (48, 10) if name == "C3" else (256, 64)
         par, ftc = base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.,
                                use_prior=(name == "C5"), alpha=2.)
+        if par["use_prior"]:
+            # V's prior constant for the power-law flux range (sampler_RHMC.py:321)
+            a = par["alpha"]
+            fmin, fmax = mag2flux(23.3) * ftc, mag2flux(15.) * ftc
+            par["V_prior_const"] = np.log(n * n) - np.log(
+                (1 - a) / (fmax ** (1 - a) - fmin ** (1 - a)))
         ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc)
         D = _image(n, [(22.5 - 2.5 * np.log10(a / ftc), b, c) for a, b, c in zip(ft, xt, yt)],
                    ftc, par["B_count"], par["fwhm_pix"], img_rng)
