@@ -699,6 +699,13 @@ int make_consts(const rhmc_params* P, Consts* c) {
   c->beta = P->beta;
   c->vc_pow = P->Vc_r_pow;
   c->vprior = P->V_prior_const;
+  c->inv_gff2 = 1.0 / c->g_ff2;
+  c->inv_g1 = 1.0 / c->g1;
+  c->Bg2 = c->B / c->g2;
+  c->inv_gxx = 1.0 / c->g_xx;
+  c->inv_two_sig2 = 1.0 / c->two_sig2;
+  c->inv_norm = 1.0 / c->psf_norm;
+  c->inv_var = 1.0 / c->var;
   c->counter_max = P->counter_max;
   c->use_prior = P->use_prior != 0;
   c->use_Vc = P->use_Vc != 0;

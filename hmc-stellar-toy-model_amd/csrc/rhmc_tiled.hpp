@@ -264,7 +264,11 @@ leapfrog_k1_tiled(LeapArgsK1 a) {
         const double nf = sf + hdt * (af + pf * ihff);
         const double nx = sx + hdt * (ax + px * ihxx);
         const double ny = sy + hdt * (ay + py * ihxx);
-        dq = nanmax2(nanmax2(fabs(f - nf), fabs(x - nx)), fabs(y - ny));
+        // max|q - q'| with np.max's NaN propagation: the sum of the three
+        // non-negative terms is NaN exactly when one of them is
+        const double a0 = fabs(f - nf), a1 = fabs(x - nx), a2 = fabs(y - ny);
+        const double sum = a0 + a1 + a2;
+        dq = (sum != sum) ? sum : fmax(fmax(a0, a1), a2);
         f = nf;
         x = nx;
         y = ny;

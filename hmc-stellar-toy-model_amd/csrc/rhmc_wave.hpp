@@ -21,6 +21,9 @@ struct Consts {
   double two_sig2, psf_norm, var;
   double g_xx, g_ff, g_ff2, g0, g1, g2, c0;
   double alpha, beta, vc_pow, vprior;
+  // reciprocals for the division-lean forms, computed once on the host (a
+  // device-side computation gets re-materialised inside the step loop)
+  double inv_gff2, inv_g1, Bg2, inv_gxx, inv_two_sig2, inv_norm, inv_var;
   int counter_max, use_prior, use_Vc, pad;
 };
 
@@ -111,15 +114,15 @@ struct LeanConsts {
 
 __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
   LeanConsts l;
-  l.inv_gff2 = 1.0 / c.g_ff2;
+  l.inv_gff2 = c.inv_gff2;
   l.c0 = c.c0;
-  l.inv_g1 = 1.0 / c.g1;
-  l.Bg2 = c.B / c.g2;
-  l.inv_gxx = 1.0 / c.g_xx;
+  l.inv_g1 = c.inv_g1;
+  l.Bg2 = c.Bg2;
+  l.inv_gxx = c.inv_gxx;
   l.f_low = c.f_low;
-  l.inv_two_sig2 = 1.0 / c.two_sig2;
-  l.inv_norm = 1.0 / c.psf_norm;
-  l.inv_var = 1.0 / c.var;
+  l.inv_two_sig2 = c.inv_two_sig2;
+  l.inv_norm = c.inv_norm;
+  l.inv_var = c.inv_var;
   return l;
 }
 
