@@ -29,6 +29,7 @@
 #include "rhmc.h"
 #include "rhmc_mh.hpp"
 #include "rhmc_tiled.hpp"
+#include "rhmc_tiled2.hpp"
 #include "rhmc_tiledk.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -630,6 +631,8 @@ struct rhmc_ctx {
 
 namespace {
 
+constexpr bool kDefaultTiled2 = false;
+
 // RHMC_KERNEL=generic / =windowed force a kernel family (the parity tests run
 // the same inputs through every path).
 bool force_generic() {
@@ -639,6 +642,13 @@ bool force_generic() {
 bool force_windowed() {
   const char* e = std::getenv("RHMC_KERNEL");
   return e && std::strcmp(e, "windowed") == 0;
+}
+// Single-star kernel variant: "tiled1" (one chain per wave) or "tiled2" (two).
+bool use_tiled2() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  if (e && std::strcmp(e, "tiled1") == 0) return false;
+  if (e && std::strcmp(e, "tiled2") == 0) return true;
+  return kDefaultTiled2;
 }
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
@@ -786,7 +796,23 @@ struct EnergyLaunch {
 
 
 template <int IMG>
+int launch_tiled2(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  int W = 4;
+  size_t lds = Tiled2<IMG>::lds_doubles(W) * sizeof(double);
+  while (lds > (size_t)ctx->max_lds && W > 1) {
+    W >>= 1;
+    lds = Tiled2<IMG>::lds_doubles(W) * sizeof(double);
+  }
+  const int64_t waves = (a.n_chains + 1) / 2;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL(leapfrog_k1_tiled2<IMG>, grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
+template <int IMG>
 int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  if (use_tiled2()) return launch_tiled2<IMG>(ctx, a, s);
   int W = 4;
   size_t lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
   while (lds > (size_t)ctx->max_lds && W > 1) {
