@@ -631,7 +631,7 @@ struct rhmc_ctx {
 
 namespace {
 
-constexpr bool kDefaultTiled2 = false;
+constexpr bool kDefaultTiled2 = true;
 
 // RHMC_KERNEL=generic / =windowed force a kernel family (the parity tests run
 // the same inputs through every path).
