@@ -518,6 +518,86 @@ __global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
   if (lane == 0) a.V[chain] = v;
 }
 
+// ---------------------------------------------------------------------------
+// Alternative integrators, windowed gradient, lanes = stars:
+//   HMC:        single_gym.run_single_HMC leapfrog, unit metric (:628-645)
+//   RHMC_NAIVE: run_single_RHMC solver="naive"     (:690-708)
+//   RHMC_LF:    run_single_RHMC solver="leap_frog" (:709-728)
+// The gradient at the end of a step is the next step's first one (same q).
+// dVdq_RHMC (:427-446): flux slot ((p_f^2 (-H_ff'/H_ff^2)) + H_ff'/H_ff + 2 H_xx'/H_xx)/2.
+__device__ __forceinline__ double dVdq_rhmc_f(double f, double pf, const Consts& c) {
+  const double hff = H_ff(f, c), hffg = H_ff_grad(f, c);
+  const double hxx = H_xx(f, c), hxxg = H_xx_grad(f, c);
+  const double t1 = (pf * pf) * (-hffg / (hff * hff));
+  const double t2 = (hffg / hff) + (2.0 * hxxg / hxx);
+  return (t1 + t2) / 2.0;
+}
+
+template <int SOLVER>
+__global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_pos) {
+  extern __shared__ double lds[];
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int K = a.K;
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const LeanConsts lc = lean_consts(c);
+  const bool owner = lane_id() < K;
+  int64_t base;
+  StarState s = load_chain(a, chain, K, owner, base);
+  const int rows = a.g.rows, cols = a.g.cols;
+  const double dt = c.dt;
+  unsigned st = 0u;
+  double gf, gx, gy;
+  win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+  for (int step = 0; step < a.n_steps; ++step) {
+    if (SOLVER == RHMC_SOLVER_HMC) {
+      const double hf = s.pf - dt * gf / 2.0, hx = s.px - dt * gx / 2.0, hy = s.py - dt * gy / 2.0;
+      s.f = s.f + dt * hf;
+      s.x = s.x + dt * hx;
+      s.y = s.y + dt * hy;
+      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+      s.pf = hf - dt * gf / 2.0;
+      s.px = hx - dt * gx / 2.0;
+      s.py = hy - dt * gy / 2.0;
+    } else if (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {
+      const double hff = H_ff(s.f, c), hxx = H_xx(s.f, c);
+      const double nf = s.f + dt * s.pf / hff, nx = s.x + dt * s.px / hxx,
+                   ny = s.y + dt * s.py / hxx;
+      const double pf_old = s.pf;
+      s.pf = s.pf - dt * (gf + dVdq_rhmc_f(s.f, s.pf, c));
+      s.px = s.px - dt * (gx + 0.0);
+      s.py = s.py - dt * (gy + 0.0);
+      if (f_pos && nf < c.f_lim) {
+        s.pf = pf_old * -1.0;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+      s.f = nf;
+      s.x = nx;
+      s.y = ny;
+      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+    } else {  // RHMC_SOLVER_RHMC_LEAPFROG
+      const double hff = H_ff(s.f, c), hxx = H_xx(s.f, c);
+      const double hf = s.pf - dt * (gf + dVdq_rhmc_f(s.f, s.pf, c)) / 2.0;
+      const double hx = s.px - dt * (gx + 0.0) / 2.0, hy = s.py - dt * (gy + 0.0) / 2.0;
+      s.f = s.f + dt * hf / hff;
+      s.x = s.x + dt * hx / hxx;
+      s.y = s.y + dt * hy / hxx;
+      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+      s.pf = hf - dt * (gf + dVdq_rhmc_f(s.f, hf, c)) / 2.0;
+      s.px = hx - dt * (gx + 0.0) / 2.0;
+      s.py = hy - dt * (gy + 0.0) / 2.0;
+      if (f_pos && s.f < c.f_lim) {
+        s.pf = hf * -1.0;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+    }
+  }
+  store_chain(a, chain, base, owner, s, 0, 0, st);
+}
+
 // Large-image gradient (windowed), one wave per chain.
 __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   extern __shared__ double lds[];
@@ -1003,6 +1083,44 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   return RHMC_OK;
 }
 
+int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* d_q,
+                     double* d_p, int64_t n, int32_t K, int32_t n_steps, int32_t f_pos,
+                     int32_t* d_st, hipStream_t s) {
+  if (solver == RHMC_SOLVER_IMPLICIT)
+    return launch_leapfrog(ctx, P, d_q, d_p, n, K, n_steps, nullptr, d_st, s);
+  if (solver < RHMC_SOLVER_HMC || solver > RHMC_SOLVER_RHMC_LEAPFROG)
+    return fail(RHMC_ERR_ARG, "unknown solver");
+  LeapArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
+  if (n == 0) return RHMC_OK;
+  a.q = d_q;
+  a.p = d_p;
+  a.fp_iters = nullptr;
+  a.status = d_st;
+  a.D = ctx->d_D;
+  a.n_chains = n;
+  a.K = K;
+  a.n_steps = n_steps;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  size_t lds;
+  int W;
+  pick_waves_win(ctx, K, &lds, &W);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+  const int fp = f_pos != 0;
+  if (solver == RHMC_SOLVER_HMC)
+    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_HMC>, grid, block, lds, s, a, fp);
+  else if (solver == RHMC_SOLVER_RHMC_NAIVE)
+    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_RHMC_NAIVE>, grid, block, lds, s, a, fp);
+  else
+    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_RHMC_LEAPFROG>, grid, block, lds, s, a,
+                       fp);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1262,6 +1380,43 @@ int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, in
     if (rec->T_chain) HIP_TRY(hipMemcpyAsync(rec->T_chain, drec.T_chain, eb, hipMemcpyDeviceToHost, ctx->stream));
     if (rec->accept) HIP_TRY(hipMemcpyAsync(rec->accept, drec.accept, ab, hipMemcpyDeviceToHost, ctx->stream));
   }
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_integrate_device(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* d_q,
+                          double* d_p, int64_t n_chains, int32_t K, int32_t n_steps,
+                          int32_t f_pos, int32_t* d_status, void* stream) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains > 0 && (!d_q || !d_p)) return fail(RHMC_ERR_ARG, "q/p is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_integrate(ctx, P, solver, d_q, d_p, n_chains, K, n_steps, f_pos, d_status, s);
+}
+
+int rhmc_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* q, double* p,
+                   int64_t n_chains, int32_t K, int32_t n_steps, int32_t f_pos,
+                   int32_t* status) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0) return RHMC_OK;
+  if (!q || !p) return fail(RHMC_ERR_ARG, "q/p is NULL");
+  const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
+  const size_t tb = (size_t)n_chains * sizeof(int32_t);
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, 2 * sb + tb + 256))) return rc;
+  char* base = (char*)ctx->scratch;
+  double* dq = (double*)base;
+  double* dp = (double*)(base + sb);
+  int32_t* dst = (int32_t*)(base + 2 * sb);
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = launch_integrate(ctx, P, solver, dq, dp, n_chains, K, n_steps, f_pos, dst,
+                             ctx->stream)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(p, dp, sb, hipMemcpyDeviceToHost, ctx->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(status, dst, tb, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RHMC_OK;
 }

@@ -31,7 +31,12 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
            "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
            "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
-           "rhmc_mh_device")
+           "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device")
+
+SOLVER_IMPLICIT = 0
+SOLVER_HMC = 1
+SOLVER_RHMC_NAIVE = 2
+SOLVER_RHMC_LEAPFROG = 3
 
 
 class RhmcParams(ctypes.Structure):
@@ -92,6 +97,12 @@ def _load():
                                          ctypes.c_int32, ctypes.c_int32]),
         "rhmc_energy": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_dp,
                                        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_integrate": (ctypes.c_int, [vp, P(RhmcParams), ctypes.c_int32, c_dp, c_dp,
+                                          ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, c_ip]),
+        "rhmc_integrate_device": (ctypes.c_int, [vp, P(RhmcParams), ctypes.c_int32, vp, vp,
+                                                 ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_int32, vp, vp]),
         "rhmc_mh": (ctypes.c_int, [vp, P(RhmcParams), c_dp, ctypes.c_int64, ctypes.c_int32,
                                    ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, c_dp, c_dp,
                                    ctypes.c_uint64, P(MhRecord)]),
@@ -300,3 +311,18 @@ class Context:
                                    ctypes.c_void_p(u_ptr or 0), ctypes.c_uint64(int(seed)),
                                    None if record is None else ctypes.byref(record),
                                    ctypes.c_void_p(stream or 0)))
+
+    def integrate(self, params, solver, q, p, n_steps, f_pos=False, return_status=False):
+        """n_steps steps of integrator `solver` (SOLVER_*); returns new (q, p)."""
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        p2 = np.array(p, dtype=np.float64, order="C", copy=True)
+        single = q2.ndim == 1
+        q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
+        p2 = p2.reshape(q2.shape)
+        st = np.zeros(q2.shape[0], np.int32)
+        _check(_lib.rhmc_integrate(self._h, ctypes.byref(params), int(solver), _dptr(q2),
+                                   _dptr(p2), q2.shape[0], q2.shape[1] // 3, int(n_steps),
+                                   int(bool(f_pos)), _iptr(st)))
+        if single:
+            q2, p2, st = q2[0], p2[0], st[0]
+        return (q2, p2, st) if return_status else (q2, p2)

@@ -297,10 +297,11 @@ class single_gym(base_class):
         self.V_chain[0] = self.V(q_tmp, f_pos=f_pos)
         self.T_chain[0] = self.T(p_tmp, np.ones_like(p_tmp))
         self.E_chain[0] = self.V_chain[0] + self.T_chain[0]
+        params = self._params()
+        ctx = self._context()
         for i in range(1, n):
-            p_half = p_tmp - self.dt * self.dVdq(q_tmp) / 2.
-            q_tmp = q_tmp + self.dt * p_half
-            p_tmp = p_half - self.dt * self.dVdq(q_tmp) / 2.
+            # one plain-leapfrog step on the GPU (rhmc_integrate, SOLVER_HMC)
+            q_tmp, p_tmp = ctx.integrate(params, capi.SOLVER_HMC, q_tmp, p_tmp, 1)
             self.q_chain[i], self.p_chain[i] = q_tmp, p_tmp
             self.V_chain[i] = self.V(q_tmp, f_pos=f_pos)
             self.T_chain[i] = self.T(p_tmp, np.ones_like(p_tmp))
@@ -310,7 +311,7 @@ class single_gym(base_class):
                         p_initial=None, counter_max=100):
         """sampler_RHMC.py:649-783.  solver="implicit" is the engine's step
         (identical math to RHMC_single_step, :729-772); "naive" and
-        "leap_frog" use the device gradient with host metric terms."""
+        "leap_frog" are the explicit RHMC integrators of rhmc_integrate."""
         if solver not in ("naive", "leap_frog", "implicit"):
             assert False
         self.Nobjs = q_model_0.shape[0]
@@ -335,24 +336,10 @@ class single_gym(base_class):
                 q_tmp, p_tmp = self.RHMC_single_step(q_tmp, p_tmp, delta=delta,
                                                      counter_max=counter_max)
                 H_diag = self.H(q_tmp)
-            elif solver == "naive":
-                q_new = q_tmp + self.dt * p_tmp / H_diag
-                p_old = p_tmp
-                p_tmp = p_tmp - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_tmp))
-                if f_pos:
-                    for k in range(self.Nobjs):
-                        if q_new[3 * k] < self.f_lim:
-                            p_tmp[3 * k] = p_old[3 * k] * -1.
-                q_tmp = q_new
-                H_diag = self.H(q_tmp)
-            else:  # leap_frog
-                p_half = p_tmp - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_tmp)) / 2.
-                q_tmp = q_tmp + self.dt * p_half / H_diag
-                p_tmp = p_half - self.dt * (self.dVdq(q_tmp) + self.dVdq_RHMC(q_tmp, p_half)) / 2.
-                if f_pos:
-                    for k in range(self.Nobjs):
-                        if q_tmp[3 * k] < self.f_lim:
-                            p_tmp[3 * k] = p_half[3 * k] * -1.
+            else:
+                sol = capi.SOLVER_RHMC_NAIVE if solver == "naive" else capi.SOLVER_RHMC_LEAPFROG
+                q_tmp, p_tmp = self._context().integrate(self._params(), sol, q_tmp, p_tmp, 1,
+                                                         f_pos=f_pos)
                 H_diag = self.H(q_tmp)
             self.q_chain[i], self.p_chain[i] = q_tmp, p_tmp
             self.V_chain[i] = self.V(q_tmp, f_pos=f_pos) - V0

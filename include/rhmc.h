@@ -25,6 +25,11 @@
  *       momentum draw p = z*sqrt(H(q)) (:1021-1022), E0 = V + T (:1025-1027),
  *       Nsteps leapfrog steps (:1053-1054), E1, accept if dE < 0 or
  *       ln u < -dE (:1072-1083) — n_iter iterations, all on the device.
+ *   rhmc_integrate / rhmc_integrate_device
+ *       the reference's other integrators, selected by RHMC_SOLVER_*:
+ *       single_gym.run_single_HMC leapfrog (sampler_RHMC.py:628-645) and
+ *       single_gym.run_single_RHMC solver="naive" (:690-708) / "leap_frog"
+ *       (:709-728); RHMC_SOLVER_IMPLICIT is RHMC_single_step.
  *   rhmc_ctx_create / rhmc_ctx_set_image
  *       the instance attribute base_class.D set by gen_mock_data
  *       (sampler_RHMC.py:77-99); uploaded once per context.
@@ -64,6 +69,14 @@ enum {
   RHMC_ERR_HIP = -2,         /* a HIP runtime call failed                */
   RHMC_ERR_NOMEM = -3,       /* device allocation failed                 */
   RHMC_ERR_UNSUPPORTED = -4  /* configuration not built into this library */
+};
+
+/* Integrators selectable through rhmc_integrate. */
+enum {
+  RHMC_SOLVER_IMPLICIT = 0,       /* RHMC_single_step (:522-566)                  */
+  RHMC_SOLVER_HMC = 1,            /* plain leapfrog, unit metric (:628-645)       */
+  RHMC_SOLVER_RHMC_NAIVE = 2,     /* explicit RHMC, "naive" (:690-708)            */
+  RHMC_SOLVER_RHMC_LEAPFROG = 3   /* explicit RHMC, "leap_frog" (:709-728)        */
 };
 
 /* Per-chain status bits written by rhmc_leapfrog (OR over all steps). */
@@ -138,6 +151,16 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
 int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
                 const double* p, double* V, double* T, int64_t n_chains,
                 int32_t K, int32_t f_pos);
+
+/* n_steps steps of integrator `solver` (RHMC_SOLVER_*) on every chain; q, p
+ * host [n_chains][3K], updated in place.  f_pos: the flux-wall momentum flip of
+ * the explicit RHMC solvers (:698-705, :719-726).  status nullable. */
+int rhmc_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* q, double* p,
+                   int64_t n_chains, int32_t K, int32_t n_steps, int32_t f_pos,
+                   int32_t* status);
+int rhmc_integrate_device(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* d_q,
+                          double* d_p, int64_t n_chains, int32_t K, int32_t n_steps,
+                          int32_t f_pos, int32_t* d_status, void* stream);
 
 /* Per-iteration records of rhmc_mh (all nullable; host pointers for rhmc_mh,
  * device pointers for rhmc_mh_device).  Row l holds the state at the START

@@ -40,6 +40,13 @@ def load_reference(ref_dir):
                     "sampler_RHMC.py", "utils.py", "samplers.py"],
                    cwd=tmp, check=True, stdout=subprocess.DEVNULL,
                    stderr=subprocess.DEVNULL)
+    # lib2to3 has no division fixer: restore Python 2's integer `/` at the one
+    # place it matters for the code exercised here (utils.py:111,
+    # convergence_stats `n = L_chain/2`, an int/int division in Python 2).
+    up = os.path.join(tmp, "utils.py")
+    src = open(up).read()
+    assert src.count("n = L_chain/2") == 1
+    open(up, "w").write(src.replace("n = L_chain/2", "n = L_chain//2"))
     np.infty = np.inf          # removed in NumPy 2 (sampler_RHMC.py:312,317,529)
     np.product = np.prod       # removed in NumPy 2 (samplers.py:911)
     os.environ.setdefault("MPLBACKEND", "Agg")
@@ -383,6 +390,60 @@ def case_mh(S, U):
     return out
 
 
+# ----------------------------------------------------------------------------
+# Case 5: alternative integrators (single_gym, sampler_RHMC.py:592-783) and
+#         post-processing (utils.py:86-209)
+# ----------------------------------------------------------------------------
+def case_solvers(S, U):
+    out = {}
+    for name, solver, stars_t, stars_m, dt, nsteps in [
+        ("hmc", None, [[17., 8.3, 7.9]], [[17.2, 8.6, 7.7]], 0.02, 60),
+        ("naive", "naive", [[19., 8.3, 7.9]], [[19.3, 8.6, 7.7]], 0.02, 60),
+        ("leap_frog", "leap_frog", [[19., 8.3, 7.9]], [[19.3, 8.6, 7.7]], 0.05, 60),
+        ("leap_frog_k2", "leap_frog", [[18., 5.3, 6.9], [19.5, 10.2, 9.1]],
+         [[18.2, 5.6, 6.6], [19.9, 10.0, 9.4]], 0.05, 40),
+        ("naive_wall", "naive", [[22.9, 8.3, 7.9]], [[22.95, 8.6, 7.7]], 0.3, 60),
+    ]:
+        np.random.seed(77)
+        g = S.single_gym(dt=0., Nsteps=0, g_xx=1., g_ff=1.)
+        g.num_rows = g.num_cols = 16
+        g.fmin = g.mag2flux_converter(20.)
+        g.fmax = g.mag2flux_converter(15.)
+        g.gen_mock_data(np.array(stars_t))
+        g.Nsteps, g.dt = nsteps, dt
+        np.random.seed(5)
+        with contextlib.redirect_stdout(io.StringIO()):
+            if solver is None:
+                g.run_single_HMC(q_model_0=np.array(stars_m), f_pos=False)
+            else:
+                g.run_single_RHMC(q_model_0=np.array(stars_m), f_pos=True, solver=solver)
+        res = dict(D=g.D, q_chain=g.q_chain, p_chain=g.p_chain, E_chain=g.E_chain,
+                   V_chain=g.V_chain, T_chain=g.T_chain, nsteps=nsteps)
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+
+    # convergence_stats / variogram / acceptance_rate on synthetic chains
+    rs = np.random.RandomState(9)
+    for name, shape, ar in [("iid", (4, 400, 3), 0.0), ("ar", (3, 501, 2), 0.9),
+                            ("ar_hi", (5, 300, 4), 0.98)]:
+        e = rs.randn(*shape)
+        x = np.empty(shape)
+        x[:, 0] = e[:, 0]
+        for t in range(1, shape[1]):
+            x[:, t] = ar * x[:, t - 1] + np.sqrt(1 - ar * ar) * e[:, t]
+        x += rs.randn(shape[0], 1, shape[2]) * 0.1       # small between-chain offsets
+        R, neff = U.convergence_stats(x, thin_rate=2, warm_up_num=10)
+        R1, neff1 = U.convergence_stats(x, thin_rate=1, warm_up_num=0)
+        chains = [x[0, :100], x[1, :100]]
+        vg = np.array([U.variogram(chains, 1, t) for t in (1, 2, 5)])
+        dec = (rs.rand(shape[0], shape[1], 1) < 0.7).astype(float)
+        acc = U.acceptance_rate(dec)
+        acc2 = U.acceptance_rate(dec, start=10, end=50)
+        out.update(pack("conv_" + name + "/", dict(x=x, R=R, neff=neff, R1=R1, neff1=neff1,
+                                                   vg=vg, dec=dec, acc=acc, acc2=acc2)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -391,7 +452,7 @@ def main():
     S, U, tmp = load_reference(args.ref)
     try:
         jobs = {"functions": case_functions, "steps": case_steps,
-                "mh": case_mh}
+                "mh": case_mh, "solvers": case_solvers}
         for name, fn in jobs.items():
             if args.only and args.only != name:
                 continue

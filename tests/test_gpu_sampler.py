@@ -143,3 +143,32 @@ def test_mh_device_rng_deterministic_and_sane(gpu_lib):
     assert 0.3 < rate <= 1.0, rate          # small-dt RHMC: high acceptance
     # chains decorrelate: not all identical after 30 iterations
     assert np.unique(q1[:, 1]).size > 32
+
+
+@pytest.mark.parametrize("name,solver", [("hmc", None), ("naive", "naive"),
+                                         ("leap_frog", "leap_frog"),
+                                         ("leap_frog_k2", "leap_frog"),
+                                         ("naive_wall", "naive")])
+def test_single_gym_alternative_integrators(gpu_lib, name, solver):
+    """run_single_HMC / run_single_RHMC(naive, leap_frog) on the GPU vs the reference."""
+    from rhmc_amd import sampler
+    z = load_golden("solvers")
+    par = R.params_from_npz(z, name + "/par_")
+    g = sampler.single_gym(dt=0., Nsteps=0, g_xx=1., g_ff=1.)
+    g.num_rows = g.num_cols = 16
+    g.fmin, g.fmax = par["fmin"], par["fmax"]
+    g.D = z[name + "/D"]
+    g.Nsteps, g.dt = int(z[name + "/nsteps"]), par["dt"]
+    q0 = z[name + "/q_chain"][0].reshape(-1, 3).copy()
+    q0[:, 0] = g.flux2mag_converter(q0[:, 0])
+    np.random.seed(5)
+    if solver is None:
+        g.run_single_HMC(q_model_0=q0, f_pos=False)
+    else:
+        g.run_single_RHMC(q_model_0=q0, f_pos=True, solver=solver)
+    assert_state_close(g.q_chain, z[name + "/q_chain"], 1e-9, "q_chain")
+    assert_state_close(g.p_chain, z[name + "/p_chain"], 1e-8, "p_chain")
+    E, Ew = g.E_chain, z[name + "/E_chain"]
+    assert np.array_equal(np.isinf(E), np.isinf(Ew))
+    fin = np.isfinite(Ew)
+    np.testing.assert_allclose(E[fin], Ew[fin], rtol=1e-9, atol=1e-7)

@@ -78,3 +78,22 @@ def test_trajectories(name, steps):
         np.testing.assert_array_equal(NQ, z["n_q"][c, :steps])
         np.testing.assert_allclose(Q, z["Q"][c, :steps + 1], rtol=1e-10, atol=1e-10)
         np.testing.assert_allclose(P, z["P"][c, :steps + 1], rtol=1e-8, atol=1e-8)
+
+
+@pytest.mark.parametrize("name,kind", [("hmc", "hmc"), ("naive", "naive"),
+                                       ("leap_frog", "lf"), ("leap_frog_k2", "lf"),
+                                       ("naive_wall", "naive")])
+def test_alternative_integrators(name, kind):
+    z = load_golden("solvers")
+    m = R.RefModel(z[name + "/D"], R.params_from_npz(z, name + "/par_"))
+    Q, P = z[name + "/q_chain"], z[name + "/p_chain"]
+    q, p = Q[0].copy(), P[0].copy()
+    for s in range(Q.shape[0] - 1):
+        if kind == "hmc":
+            q, p = m.hmc_step(q, p)
+        elif kind == "naive":
+            q, p = m.rhmc_naive_step(q, p, True)
+        else:
+            q, p = m.rhmc_leapfrog_step(q, p, True)
+        np.testing.assert_allclose(q, Q[s + 1], rtol=1e-12, atol=1e-12)
+        np.testing.assert_allclose(p, P[s + 1], rtol=1e-10, atol=1e-10)
