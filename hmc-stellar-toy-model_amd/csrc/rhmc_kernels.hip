@@ -27,6 +27,7 @@
 #include <string>
 
 #include "rhmc.h"
+#include "rhmc_datagen.hpp"
 #include "rhmc_mh.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
@@ -1121,6 +1122,37 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   return RHMC_OK;
 }
 
+// Model image / Poisson realisations (rhmc_datagen.hpp) into d_out
+// [max(n_real,1)][rows][cols].
+int launch_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int32_t K,
+                     int32_t rows, int32_t cols, int32_t n_real, uint64_t seed, double* d_out,
+                     hipStream_t s) {
+  DataArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  if (K < 0 || K > (1 << 20)) return fail(RHMC_ERR_ARG, "K must be in [0, 2^20]");
+  if (rows < 1 || cols < 1) return fail(RHMC_ERR_ARG, "rows/cols must be >= 1");
+  if (n_real < 0) return fail(RHMC_ERR_ARG, "n_real < 0");
+  if (K > 0 && !d_q) return fail(RHMC_ERR_ARG, "q is NULL");
+  if (!d_out) return fail(RHMC_ERR_ARG, "out is NULL");
+  const int64_t npix = (int64_t)rows * cols;
+  const int64_t total = npix * (n_real > 0 ? n_real : 1);
+  if (total > ((int64_t)1 << 36)) return fail(RHMC_ERR_ARG, "rows*cols*n_real too large");
+  a.q = d_q;
+  a.out = d_out;
+  a.K = K;
+  a.rows = rows;
+  a.cols = cols;
+  a.poisson = n_real > 0;
+  a.n_real = n_real;
+  a.seed = seed;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const dim3 grid((unsigned)((total + 255) / 256)), block(256);
+  hipLaunchKernelGGL(datagen_kernel, grid, block, 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -1178,7 +1210,7 @@ int rhmc_ctx_create(int device, const double* D, int32_t rows, int32_t cols, rhm
     delete ctx;
     return fail(RHMC_ERR_HIP, "hipStreamCreate failed");
   }
-  int rc = rhmc_ctx_set_image(ctx, D, rows, cols);
+  int rc = D ? rhmc_ctx_set_image(ctx, D, rows, cols) : RHMC_OK;  // NULL: no image yet
   if (rc) {
     std::string keep = g_err;
     rhmc_ctx_destroy(ctx);
@@ -1417,6 +1449,58 @@ int rhmc_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* 
   HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(p, dp, sb, hipMemcpyDeviceToHost, ctx->stream));
   if (status) HIP_TRY(hipMemcpyAsync(status, dst, tb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_gen_image_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int32_t K,
+                          int32_t rows, int32_t cols, int32_t n_real, uint64_t seed,
+                          double* d_out, void* stream) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_gen_image(ctx, P, d_q, K, rows, cols, n_real, seed, d_out, s);
+}
+
+int rhmc_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* q, int32_t K, int32_t rows,
+                   int32_t cols, int32_t n_real, uint64_t seed, double* out, int32_t install) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!out && !install) return fail(RHMC_ERR_ARG, "out is NULL and install == 0");
+  if (K < 0 || K > (1 << 20)) return fail(RHMC_ERR_ARG, "K must be in [0, 2^20]");
+  if (K > 0 && !q) return fail(RHMC_ERR_ARG, "q is NULL");
+  if (rows < 1 || cols < 1) return fail(RHMC_ERR_ARG, "rows/cols must be >= 1");
+  if (n_real < 0) return fail(RHMC_ERR_ARG, "n_real < 0");
+  if (install && rows != cols)
+    return fail(RHMC_ERR_ARG, "rows must equal cols to install the image");
+  if (install && (int64_t)rows * cols > (1 << 26)) return fail(RHMC_ERR_ARG, "image too large");
+  const int64_t npix = (int64_t)rows * cols;
+  const int64_t nimg = n_real > 0 ? n_real : 1;
+  if (npix * nimg > ((int64_t)1 << 36)) return fail(RHMC_ERR_ARG, "rows*cols*n_real too large");
+  const size_t qb = ((size_t)3 * K * sizeof(double) + 255) & ~(size_t)255;
+  const size_t ob = (size_t)(npix * nimg) * sizeof(double);
+  HIP_TRY(hipSetDevice(ctx->device));
+  int rc = ensure_scratch(ctx, qb + ob + 256);
+  if (rc) return rc;
+  double* dq = (double*)ctx->scratch;
+  double* dout = (double*)((char*)ctx->scratch + qb);
+  if (K > 0)
+    HIP_TRY(hipMemcpyAsync(dq, q, (size_t)3 * K * sizeof(double), hipMemcpyHostToDevice,
+                           ctx->stream));
+  if ((rc = launch_gen_image(ctx, P, dq, K, rows, cols, n_real, seed, dout, ctx->stream)))
+    return rc;
+  if (install) {  // image 0 becomes the context's data image (stays on the device)
+    const size_t bytes = (size_t)npix * sizeof(double);
+    if (ctx->d_D && (int64_t)ctx->rows * ctx->cols != npix) {
+      HIP_TRY(hipStreamSynchronize(ctx->stream));
+      HIP_TRY(hipFree(ctx->d_D));
+      ctx->d_D = nullptr;
+    }
+    if (!ctx->d_D && hipMalloc(&ctx->d_D, bytes) != hipSuccess)
+      return fail(RHMC_ERR_NOMEM, "hipMalloc image failed");
+    HIP_TRY(hipMemcpyAsync(ctx->d_D, dout, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    ctx->rows = rows;
+    ctx->cols = cols;
+  }
+  if (out) HIP_TRY(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RHMC_OK;
 }

@@ -31,7 +31,8 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
            "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
            "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
-           "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device")
+           "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
+           "rhmc_gen_image", "rhmc_gen_image_device")
 
 SOLVER_IMPLICIT = 0
 SOLVER_HMC = 1
@@ -109,6 +110,12 @@ def _load():
         "rhmc_mh_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                           ctypes.c_uint64, P(MhRecord), vp]),
+        "rhmc_gen_image": (ctypes.c_int, [vp, P(RhmcParams), c_dp, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, c_dp,
+                                          ctypes.c_int32]),
+        "rhmc_gen_image_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int32,
+                                                 ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                                 ctypes.c_uint64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -172,14 +179,20 @@ class Context:
     """One GPU + one data image (rhmc_ctx)."""
 
     def __init__(self, D, device=0):
-        D = _f64(D, "D")
-        if D.ndim != 2:
-            raise ValueError("D must be 2-D")
+        """D: the data image, or None for a context whose image comes from
+        gen_image(..., install=True)."""
         h = ctypes.c_void_p()
-        _check(_lib.rhmc_ctx_create(int(device), _dptr(D), D.shape[0], D.shape[1],
-                                    ctypes.byref(h)))
+        if D is None:
+            _check(_lib.rhmc_ctx_create(int(device), None, 0, 0, ctypes.byref(h)))
+            self.shape = None
+        else:
+            D = _f64(D, "D")
+            if D.ndim != 2:
+                raise ValueError("D must be 2-D")
+            _check(_lib.rhmc_ctx_create(int(device), _dptr(D), D.shape[0], D.shape[1],
+                                        ctypes.byref(h)))
+            self.shape = D.shape
         self._h = h
-        self.shape = D.shape
         self.device = device
 
     @property
@@ -326,3 +339,24 @@ class Context:
         if single:
             q2, p2, st = q2[0], p2[0], st[0]
         return (q2, p2, st) if return_status else (q2, p2)
+
+    def gen_image(self, params, q, rows, cols, n_real=0, seed=0, install=False):
+        """Model image (n_real=0, gen_model) or n_real Poisson realisations of it
+        (gen_mock_data / gen_noise_profile) for stars q [K, 3] (flux in counts,
+        x, y).  Returns [rows, cols] or [n_real, rows, cols]; install=True also
+        makes image 0 this context's data image."""
+        qq = np.ascontiguousarray(np.asarray(q, dtype=np.float64).reshape(-1, 3))
+        K = qq.shape[0]
+        out = np.empty((n_real, rows, cols) if n_real > 0 else (rows, cols))
+        _check(_lib.rhmc_gen_image(self._h, ctypes.byref(params), _dptr(qq) if K else None,
+                                   K, int(rows), int(cols), int(n_real),
+                                   ctypes.c_uint64(int(seed)), _dptr(out), int(bool(install))))
+        if install:
+            self.shape = (rows, cols)
+        return out
+
+    def gen_image_device(self, params, q_ptr, K, rows, cols, n_real, seed, out_ptr, stream=None):
+        _check(_lib.rhmc_gen_image_device(self._h, ctypes.byref(params),
+                                          ctypes.c_void_p(q_ptr or 0), int(K), int(rows),
+                                          int(cols), int(n_real), ctypes.c_uint64(int(seed)),
+                                          ctypes.c_void_p(out_ptr), ctypes.c_void_p(stream or 0)))

@@ -101,8 +101,25 @@ class base_class(object):
             raise ValueError("D has shape %s but num_rows/num_cols are %d/%d"
                              % (self._D.shape, self.num_rows, self.num_cols))
 
-    def gen_mock_data(self, q_true=None, return_data=False):
-        """sampler_RHMC.py:77-99 (global NumPy RNG, row-major Poisson draws)."""
+    def gen_mock_data(self, q_true=None, return_data=False, rng="numpy", seed=0):
+        """sampler_RHMC.py:77-99.  rng="numpy": the reference's global NumPy
+        RNG, row-major Poisson draws (bit-identical data).  rng="device": model
+        and Poisson draw on the GPU (rhmc_gen_image, Philox keyed by `seed`);
+        without return_data the image is installed in the device context
+        directly (no host->device upload) and mirrored to .D."""
+        if rng == "device":
+            self._check_square()
+            ctx = self._gen_context()
+            data = ctx.gen_image(self._gen_params(), self._counts(q_true), self.num_rows,
+                                 self.num_cols, n_real=1, seed=seed,
+                                 install=not return_data)[0]
+            if return_data:
+                return data
+            self._D = np.ascontiguousarray(data)
+            self._ctx_shape = data.shape
+            return None
+        if rng != "numpy":
+            raise ValueError("rng must be 'numpy' or 'device'")
         data = np.ones((self.num_rows, self.num_cols), dtype=float) * self.B_count
         for i in range(q_true.shape[0]):
             mag, x, y = q_true[i]
@@ -113,8 +130,12 @@ class base_class(object):
             return data
         self.D = data
 
-    def gen_model(self, q_model):
-        """sampler_RHMC.py:101-116."""
+    def gen_model(self, q_model, device=False):
+        """sampler_RHMC.py:101-116 (device=True: rhmc_gen_image, n_real=0)."""
+        if device:
+            self._check_square()
+            return self._gen_context().gen_image(self._gen_params(), self._counts(q_model),
+                                                 self.num_rows, self.num_cols, n_real=0)
         model = np.ones((self.num_rows, self.num_cols), dtype=float) * self.B_count
         for i in range(q_model.shape[0]):
             mag, x, y = q_model[i]
@@ -122,15 +143,50 @@ class base_class(object):
                 self.num_rows, self.num_cols, x, y, FWHM=self.PSF_FWHM_pix)
         return model
 
-    def gen_noise_profile(self, q_true, N_trial=1000, sig_fac=10):
-        """sampler_RHMC.py:118-145 (`normed=` is NumPy's `density=` today)."""
-        truth = self.gen_model(q_true)
-        res = np.vstack([poisson_realization(truth) - truth for _ in range(N_trial)]).ravel()
+    def gen_noise_profile(self, q_true, N_trial=1000, sig_fac=10, rng="numpy", seed=0):
+        """sampler_RHMC.py:118-145 (`normed=` is NumPy's `density=` today).
+        rng="device": the N_trial realisations are one rhmc_gen_image launch."""
+        if rng == "device":
+            self._check_square()
+            ctx = self._gen_context()
+            gp = self._gen_params()
+            q = self._counts(q_true)
+            truth = ctx.gen_image(gp, q, self.num_rows, self.num_cols, n_real=0)
+            res = (ctx.gen_image(gp, q, self.num_rows, self.num_cols, n_real=N_trial,
+                                 seed=seed) - truth).ravel()
+        elif rng == "numpy":
+            truth = self.gen_model(q_true)
+            res = np.vstack([poisson_realization(truth) - truth
+                             for _ in range(N_trial)]).ravel()
+        else:
+            raise ValueError("rng must be 'numpy' or 'device'")
         sig = np.sqrt(self.B_count)
         bins = np.arange(-sig_fac * sig, sig_fac * sig, sig / 5.)
         hist, _ = np.histogram(res, bins=bins, density=True)
         self.hist_noise = hist
         self.centers_noise = (bins[1:] + bins[:-1]) / 2.
+
+    def _counts(self, q_mag):
+        """(K, 3) mag, x, y -> (K, 3) counts, x, y (like format_q, :209)."""
+        q = np.array(q_mag, dtype=float).reshape(-1, 3)
+        q[:, 0] = [self.mag2flux_converter(m) for m in q[:, 0]]
+        return q
+
+    def _check_square(self):
+        if self.num_rows != self.num_cols:
+            raise ValueError("square images only (gauss_PSF, utils.py:481-483)")
+
+    def _gen_context(self):
+        if self._ctx is None:
+            self._ctx = capi.Context(None, device=self.device)
+            self._ctx_shape = None        # .D (if any) is uploaded on first use
+        return self._ctx
+
+    def _gen_params(self):
+        """rhmc_gen_image reads B_count and PSF_FWHM_pix only."""
+        return capi.make_params(dt=self.dt, delta=1e-6, counter_max=1, B_count=self.B_count,
+                                f_lim=self.f_lim, f_low=0., fwhm_pix=self.PSF_FWHM_pix,
+                                g_xx=1., g_ff=1., g_ff2=1., g0=self.g0, g1=self.g1, g2=self.g2)
 
     def mag2flux_converter(self, mag):
         """sampler_RHMC.py:147-152"""

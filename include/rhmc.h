@@ -33,6 +33,10 @@
  *   rhmc_ctx_create / rhmc_ctx_set_image
  *       the instance attribute base_class.D set by gen_mock_data
  *       (sampler_RHMC.py:77-99); uploaded once per context.
+ *   rhmc_gen_image / rhmc_gen_image_device
+ *       base_class.gen_model (sampler_RHMC.py:101-116), gen_mock_data
+ *       (:77-99, Poisson draw utils.py:488-496) and the N_trial realisations
+ *       of gen_noise_profile (:118-144), on the device.
  *   rhmc_params
  *       the instance attributes the step reads: dt, g_xx,
  *       g_ff, g_ff2, g0, g1, g2, B_count, f_lim, mB (-> f_low),
@@ -189,6 +193,28 @@ int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, in
 int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
                    int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
                    const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream);
+
+/*
+ * Data generation.  q: [K][3] (flux in counts, x, y), K >= 0.  n_real == 0:
+ * the model image B_count + sum_k f_k PSF_k (gen_model, sampler_RHMC.py:101-116;
+ * per pixel exp(-((i+.5-x)^2 + (j+.5-y)^2) / (2 sigma^2)) / (2 pi sigma^2),
+ * utils.py:475-486) into out [rows][cols].  n_real >= 1: n_real independent
+ * Poisson realisations of it (gen_mock_data :77-99 / gen_noise_profile
+ * :130-133) into out [n_real][rows][cols]; the Poisson sampler is NumPy's
+ * legacy algorithm (multiplication below lam 10, PTRS above) on Philox-4x32-10
+ * keyed by `seed` and the pixel index — the same distribution as the
+ * reference, not the same stream.  Only P->B_count and P->fwhm_pix are read
+ * (P->reserved must be 0).  install != 0 makes image 0 the context's data
+ * image without a host round trip (rows == cols); out may then be NULL.
+ * rhmc_ctx_create accepts D == NULL for a context that gets its image here.
+ */
+int rhmc_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* q, int32_t K,
+                   int32_t rows, int32_t cols, int32_t n_real, uint64_t seed, double* out,
+                   int32_t install);
+/* Device pointers, asynchronous on `stream`; d_out [max(n_real,1)][rows][cols]. */
+int rhmc_gen_image_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int32_t K,
+                          int32_t rows, int32_t cols, int32_t n_real, uint64_t seed,
+                          double* d_out, void* stream);
 
 #ifdef __cplusplus
 }

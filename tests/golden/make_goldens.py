@@ -444,6 +444,45 @@ def case_solvers(S, U):
     return out
 
 
+def case_datagen(S, U):
+    """gen_model (sampler_RHMC.py:101-116), gen_mock_data (:77-99) and
+    gen_noise_profile (:118-144) outputs.  gen_noise_profile calls
+    np.histogram(normed=True), removed in NumPy 2: it is run with a shim that
+    maps normed to density (equal-width bins: the same normalisation)."""
+    out = {}
+    cases = [("k1_48", "multi", 48, [[19., 24.3, 23.8]]),
+             ("k1_32", "single", 32, [[17.5, 16.2, 15.7]]),
+             ("k2_16", "single", 16, [[18., 5.3, 6.9], [19.5, 10.2, 9.1]])]
+    g = make_gym(S, "multi", 48)
+    np.random.seed(12)
+    K = 10
+    mags = 15. + 8.3 * np.random.rand(K)
+    xy = np.random.rand(K, 2) * 46. + 1.
+    cases.append(("k10_48", "multi", 48, np.column_stack([mags, xy]).tolist()))
+    orig_hist = np.histogram
+
+    def hist_shim(a, bins=10, range=None, normed=None, weights=None, density=None):
+        return orig_hist(a, bins=bins, range=range, weights=weights,
+                         density=bool(normed) or bool(density))
+    for name, cls, n, stars in cases:
+        g = make_gym(S, cls, n)
+        qm = np.array(stars, dtype=float)
+        model = g.gen_model(qm)
+        np.random.seed(31)
+        D = g.gen_mock_data(qm, return_data=True)
+        np.random.seed(32)
+        np.histogram = hist_shim
+        try:
+            g.gen_noise_profile(qm, N_trial=8, sig_fac=10)
+        finally:
+            np.histogram = orig_hist
+        out.update(pack(name + "/", dict(stars=qm, q=stars_to_q(g, qm.copy()).reshape(-1, 3),
+                                         model=model, D=D, hist=g.hist_noise,
+                                         centers=g.centers_noise)))
+        out.update(pack(name + "/par_", gym_params(g)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -452,7 +491,8 @@ def main():
     S, U, tmp = load_reference(args.ref)
     try:
         jobs = {"functions": case_functions, "steps": case_steps,
-                "mh": case_mh, "solvers": case_solvers}
+                "mh": case_mh, "solvers": case_solvers,
+                "datagen": case_datagen}
         for name, fn in jobs.items():
             if args.only and args.only != name:
                 continue

@@ -97,3 +97,13 @@ def test_alternative_integrators(name, kind):
             q, p = m.rhmc_leapfrog_step(q, p, True)
         np.testing.assert_allclose(q, Q[s + 1], rtol=1e-12, atol=1e-12)
         np.testing.assert_allclose(p, P[s + 1], rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["k1_48", "k1_32", "k2_16", "k10_48"])
+def test_model_image(name):
+    """oracle model_image == the reference's gen_model (sampler_RHMC.py:101-116)."""
+    z = load_golden("datagen")
+    par = R.params_from_npz(z, name + "/par_")
+    got = R.model_image(int(par["rows"]), int(par["cols"]), z[name + "/q"], par["B_count"],
+                        par["fwhm_pix"])
+    np.testing.assert_array_equal(got, z[name + "/model"])

@@ -79,3 +79,23 @@ def test_quirk_errors_like_reference():
         g2._params(for_energy=True)
     with pytest.raises(NotImplementedError):
         g2.run_RHMC(np.array([[19., 24., 24.]]), P_move=[0.6, 0.2, 0.2])
+
+
+@pytest.mark.parametrize("name,cls", [("k1_48", "multi"), ("k1_32", "single"),
+                                      ("k2_16", "single"), ("k10_48", "multi")])
+def test_datagen_numpy_path_matches_reference(name, cls):
+    """gen_model / gen_mock_data / gen_noise_profile with the NumPy stream are the
+    reference's outputs bit for bit (goldens: make_goldens.py case_datagen)."""
+    z = load_golden("datagen")
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym_from(par, cls)
+    stars = z[name + "/stars"]
+    np.testing.assert_array_equal(g.gen_model(stars), z[name + "/model"])
+    np.random.seed(31)
+    np.testing.assert_array_equal(g.gen_mock_data(stars, return_data=True), z[name + "/D"])
+    np.random.seed(32)
+    g.gen_noise_profile(stars, N_trial=8, sig_fac=10)
+    np.testing.assert_array_equal(g.hist_noise, z[name + "/hist"])
+    np.testing.assert_array_equal(g.centers_noise, z[name + "/centers"])
+    with pytest.raises(ValueError):
+        g.gen_mock_data(stars, rng="bogus")
