@@ -100,6 +100,65 @@ def load_pmc(workload):
         return {}
 
 
+def bench_datagen(args, wl, P, ctx, dev, stream, world, rank):
+    """--mode datagen: n_real Poisson realisations of the workload's true model
+    image per launch (gen_noise_profile's inner loop, sampler_RHMC.py:130-133).
+    Algorithmic bytes per pixel: the 8-byte write (the model is recomputed
+    from the K stars in registers)."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from rhmc_amd import shard
+    rows, cols = wl.D.shape
+    stars = np.ascontiguousarray(wl.q0[0].reshape(-1, 3))
+    n_real = args.n_real
+    dq = torch.from_numpy(stars).to(dev)
+    out = torch.empty((n_real, rows, cols), dtype=torch.float64, device=dev)
+
+    def launch(i):
+        ctx.gen_image_device(P, dq.data_ptr(), wl.K, rows, cols, n_real, 77 + i + 1000 * rank,
+                             out.data_ptr(), stream=stream.cuda_stream)
+    for i in range(args.warmup):
+        launch(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i, (a, b) in enumerate(ev):
+        a.record(stream)
+        launch(args.warmup + i)
+        b.record(stream)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        wall = shard.max_over_ranks(wall)
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    draws = n_real * rows * cols
+    achieved = 8.0 * draws / (launch_ms * 1e-3) / 1e9
+    res = {
+        "metric": "Poisson pixel draws/sec (device gen_mock_data / gen_noise_profile)",
+        "value": draws * world * args.steps / wall, "unit": "pixel-draws/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": wall / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic (%s true stars)" % wl.name,
+        "config": {"workload": "%s model image %dx%d, K=%d, %d realisations per launch"
+                               % (wl.name, rows, cols, wl.K, n_real), "mode": "datagen"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "alg_bytes_per_pixel": 8, "kernel_ms": launch_ms},
+        "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -111,10 +170,16 @@ def main():
                     help="total chains split over the ranks (strong scaling, e.g. C4 = 2^20)")
     ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", choices=("leapfrog", "mh"), default="leapfrog",
+    ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "datagen"),
+                    default="leapfrog",
                     help="mh: whole MH iterations on device (momentum draw, V+T, accept; "
-                         "Philox RNG); one bench step = --mh-iter iterations of --leap steps")
+                         "Philox RNG); one bench step = --mh-iter iterations of --leap steps. "
+                         "integrate: --solver's explicit integrator (rhmc_integrate). "
+                         "datagen: --n-real Poisson realisations of the workload's model "
+                         "image (rhmc_gen_image)")
     ap.add_argument("--mh-iter", type=int, default=10)
+    ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
+    ap.add_argument("--n-real", type=int, default=1000)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,7 +196,7 @@ def main():
         wl = workloads.make(args.workload, n_chains=args.chains, seed_offset=rank)
     # CPU baseline first: forked workers must not inherit an initialised GPU.
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and world == 1 and not args.no_cpu and args.mode == "leapfrog":
         cpu = cpu_baseline(wl)
 
     import torch
@@ -154,12 +219,21 @@ def main():
     # timing events are recorded on it.
     stream = torch.cuda.Stream(dev)
 
+    if args.mode == "datagen":
+        return bench_datagen(args, wl, P, ctx, dev, stream, world, rank)
     if args.mode == "mh":
         leap = args.leap or 10
 
         def launch():
             ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap, f_pos=True,
                           seed=1234 + rank, stream=stream.cuda_stream)
+    elif args.mode == "integrate":
+        solver = {"hmc": capi.SOLVER_HMC, "naive": capi.SOLVER_RHMC_NAIVE,
+                  "leap_frog": capi.SOLVER_RHMC_LEAPFROG}[args.solver]
+
+        def launch():
+            ctx.integrate_device(P, solver, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
+                                 f_pos=True, status_ptr=st.data_ptr(), stream=stream.cuda_stream)
     else:
         def launch():
             ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
@@ -202,7 +276,8 @@ def main():
     npix = wl.D.size
     bpu = alg_bytes_per_step(npix, wl.K)
     achieved = bpu * chain_steps / (launch_ms * 1e-3) / 1e9
-    pmc = load_pmc(wl.name)
+    # PMC summaries describe the implicit leapfrog kernel only
+    pmc = load_pmc(wl.name) if args.mode == "leapfrog" else {}
     traffic = pmc.get("hbm_bytes_per_launch")
     if traffic is not None and pmc.get("chain_steps_per_dispatch") not in (None, chain_steps):
         traffic = traffic * chain_steps / pmc["chain_steps_per_dispatch"]
@@ -225,6 +300,7 @@ def main():
                    "chains_per_gpu": wl.n_chains, "total_chains": total_chains,
                    "image": list(wl.D.shape), "K": wl.K,
                    "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
+                   "solver": args.solver if args.mode == "integrate" else "implicit",
                    "parallelism": "chain-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

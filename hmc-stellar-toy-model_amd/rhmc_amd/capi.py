@@ -340,6 +340,15 @@ class Context:
             q2, p2, st = q2[0], p2[0], st[0]
         return (q2, p2, st) if return_status else (q2, p2)
 
+    def integrate_device(self, params, solver, q_ptr, p_ptr, n_chains, K, n_steps, f_pos=False,
+                         status_ptr=None, stream=None):
+        """Device-pointer rhmc_integrate (asynchronous on `stream`)."""
+        _check(_lib.rhmc_integrate_device(self._h, ctypes.byref(params), int(solver),
+                                          ctypes.c_void_p(q_ptr), ctypes.c_void_p(p_ptr),
+                                          int(n_chains), int(K), int(n_steps),
+                                          int(bool(f_pos)), ctypes.c_void_p(status_ptr or 0),
+                                          ctypes.c_void_p(stream or 0)))
+
     def gen_image(self, params, q, rows, cols, n_real=0, seed=0, install=False):
         """Model image (n_real=0, gen_model) or n_real Poisson realisations of it
         (gen_mock_data / gen_noise_profile) for stars q [K, 3] (flux in counts,
