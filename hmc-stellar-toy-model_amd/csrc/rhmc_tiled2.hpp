@@ -82,38 +82,43 @@ struct Tiled2 {
     }
     wave_lds_sync();
 
-    double srow[TR], scol[TC];
+    // s_ij = D_ij / Lambda_ij - 1 and, by separability (PSF_ij = ex_i ey_j),
+    //   sum_ij PSF s      = sum_i ex_i R_i,        R_i = sum_j ey_j s_ij
+    //   sum_ij PSF s dx_i = sum_i ex_i dx_i R_i
+    //   sum_ij PSF s dy_j = sum_j ey_j dy_j C_j,   C_j = sum_i ex_i s_ij
+    // so the pixel loop never forms PSF_ij: Lambda = fma(f ex_i, ey_j, B), one
+    // reciprocal per pixel pair (+1 Newton step), s, and two fmas.
+    double fex[TR], R[TR], C[TC];
 #pragma unroll
-    for (int k = 0; k < TR; ++k) srow[k] = 0.0;
+    for (int k = 0; k < TR; ++k) {
+      fex[k] = f * ex[k];
+      R[k] = 0.0;
+    }
 #pragma unroll
-    for (int k = 0; k < TC; ++k) scol[k] = 0.0;
+    for (int k = 0; k < TC; ++k) C[k] = 0.0;
 #pragma unroll
     for (int pp = 0; pp < TR * TC; pp += 2) {
       const int i1 = pp / TC, j1 = pp % TC, i2 = (pp + 1) / TC, j2 = (pp + 1) % TC;
       const double d1 = sDm[pp * 32], d2 = sDm[(pp + 1) * 32];
-      const double psf1 = ex[i1] * ey[j1], psf2 = ex[i2] * ey[j2];
-      const double l1 = fma(f, psf1, c.B), l2 = fma(f, psf2, c.B);  // :373-376
+      const double l1 = fma(fex[i1], ey[j1], c.B), l2 = fma(fex[i2], ey[j2], c.B);  // :373-376
       const double L = l1 * l2;
       double r = __builtin_amdgcn_rcp(L);
       r = fma(r, fma(-L, r, 1.0), r);
-      const double r1 = l2 * r, r2 = l1 * r;
-      double q1 = d1 * r1, q2 = d2 * r2;                            // D/Lambda (:379)
-      q1 = fma(r1, fma(-l1, q1, d1), q1);
-      q2 = fma(r2, fma(-l2, q2, d2), q2);
-      const double w1 = fma(psf1, q1, -psf1), w2 = fma(psf2, q2, -psf2);
-      srow[i1] += w1;
-      scol[j1] += w1;
-      srow[i2] += w2;
-      scol[j2] += w2;
+      const double s1 = fma(d1, l2 * r, -1.0), s2 = fma(d2, l1 * r, -1.0);  // D/Lambda - 1 (:379)
+      R[i1] = fma(ey[j1], s1, R[i1]);
+      C[j1] = fma(ex[i1], s1, C[j1]);
+      R[i2] = fma(ey[j2], s2, R[i2]);
+      C[j2] = fma(ex[i2], s2, C[j2]);
     }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
     for (int k = 0; k < TR; ++k) {
-      a0 += srow[k];
-      a1 = fma(srow[k], dx[k], a1);
+      const double t = ex[k] * R[k];
+      a0 += t;
+      a1 = fma(t, dx[k], a1);
     }
 #pragma unroll
-    for (int k = 0; k < TC; ++k) a2 = fma(scol[k], dy[k], a2);
+    for (int k = 0; k < TC; ++k) a2 = fma(ey[k] * C[k], dy[k], a2);
     const double s0 = half_sum_dpp(a0);
     const double s1 = half_sum_dpp(a1);
     const double s2 = half_sum_dpp(a2);
