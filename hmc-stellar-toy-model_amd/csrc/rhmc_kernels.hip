@@ -31,7 +31,9 @@
 #include "rhmc_mh.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
+#include "rhmc_tiledg.hpp"
 #include "rhmc_tiledk.hpp"
+#include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 
@@ -732,6 +734,38 @@ bool use_tiled2() {
   return kDefaultTiled2;
 }
 
+// The 32-pixel windows (rhmc_tiledw.hpp, rhmc_windowed.hpp) drop pixel
+// centres >= 15.5 px from a star; exact to fp64 only while their PSF factor
+// exp(-15.5^2 / (2 sigma^2)) <= 2^-70, i.e. sigma <= 1.574 px (reference: 1.487).
+bool window_exact(const Consts& c) { return 15.5 * 15.5 * c.inv_two_sig2 >= 48.5; }
+
+int window_unsupported() {
+  return fail(RHMC_ERR_UNSUPPORTED,
+              "PSF wider than the 32-pixel window allows (sigma > 1.574 px) for a configuration "
+              "that needs the windowed kernels (K > 16 or image larger than LDS)");
+}
+
+// RHMC_KERNEL=tiledw forces the windowed single-star kernel, "tiled2"/"tiled1"
+// and the generic-LPC names below force full-image kernels.
+bool force_full_image_k1() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  return e && std::strcmp(e, "tiledw") != 0 && std::strncmp(e, "tiled", 5) == 0;
+}
+
+// RHMC_KERNEL=tiled4 / tiled4w1 / tiledg32 / tiledg64: the generic-LPC kernel
+// with 16 (2 or 1 waves/EU budget), 32, 64 lanes per chain; 0 = not selected.
+int tiledg_lanes() {
+  const char* e = std::getenv("RHMC_KERNEL");
+  if (!e) return 0;
+  if (std::strcmp(e, "tiled4") == 0) return 16;
+  if (std::strcmp(e, "tiled4w1") == 0) return 17;
+  if (std::strcmp(e, "tiledg32") == 0) return 32;
+  if (std::strcmp(e, "tiledg64") == 0) return 64;
+  if (std::strcmp(e, "prof16") == 0) return 116;   // phase-timing builds (tools only)
+  if (std::strcmp(e, "prof32") == 0) return 132;
+  return 0;
+}
+
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
 constexpr int kMaxK = 64;          // windowed kernel: lanes = stars
 
@@ -891,8 +925,32 @@ int launch_tiled2(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
+// Generic-LPC single-star kernel (rhmc_tiledg.hpp).
+template <int IMG, int LPC, int WPE, bool PROF = false>
+int launch_tiledg(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  using TL = TiledG<IMG, LPC>;
+  int W = 4;
+  size_t lds = TL::lds_doubles(W) * sizeof(double);
+  while (lds > (size_t)ctx->max_lds && W > 1) {
+    W >>= 1;
+    lds = TL::lds_doubles(W) * sizeof(double);
+  }
+  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_k1_tiledg<IMG, LPC, WPE, PROF>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 template <int IMG>
 int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  const int lpc = tiledg_lanes();
+  if (lpc == 16) return launch_tiledg<IMG, 16, 2>(ctx, a, s);
+  if (lpc == 17) return launch_tiledg<IMG, 16, 1>(ctx, a, s);
+  if (lpc == 32) return launch_tiledg<IMG, 32, 2>(ctx, a, s);
+  if (lpc == 64) return launch_tiledg<IMG, 64, 2>(ctx, a, s);
+  if (lpc == 116) return launch_tiledg<IMG, 16, 2, true>(ctx, a, s);
+  if (lpc == 132) return launch_tiledg<IMG, 32, 2, true>(ctx, a, s);
   if (use_tiled2()) return launch_tiled2<IMG>(ctx, a, s);
   int W = 4;
   size_t lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
@@ -906,6 +964,23 @@ int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
+template <int IMG>
+int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  using TL = TiledW<IMG>;
+  int W = 4;
+  size_t lds = TL::lds_doubles(W) * sizeof(double);
+  while (lds > (size_t)ctx->max_lds && W > 1) {
+    W >>= 1;
+    lds = TL::lds_doubles(W) * sizeof(double);
+  }
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+  const int64_t waves = (a.n_chains + 1) / 2;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL(leapfrog_k1_tiledw<IMG>, grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 // V (and optionally T) of n chains on device buffers, async on `s`.
 int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const double* d_p,
                   double* d_V, double* d_T, int64_t n, int K, int f_pos, hipStream_t s) {
@@ -915,6 +990,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   int W;
   int rc;
   const bool win = use_windowed(ctx, K);
+  if (win && !window_exact(c)) return window_unsupported();
   if (win)
     pick_waves_win(ctx, K, &lds, &W);
   else if ((rc = pick_waves(ctx, K, &lds, &W)))
@@ -970,8 +1046,11 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   if (n_chains == 0) return RHMC_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const int side = ctx->rows;
-  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() && !force_windowed() &&
-      (side == 16 || side == 32 || side == 48 || side == 64)) {
+  const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
+                  !force_windowed();
+  const bool k1w = k1 && window_exact(a.c) && !force_full_image_k1() &&
+                   (side == 48 || side == 64 || side == 96 || side == 128);
+  if (k1w || (k1 && (side == 16 || side == 32 || side == 48 || side == 64))) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -984,6 +1063,14 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.cols = ctx->cols;
     t.pad = 0;
     t.c = a.c;
+    if (k1w) {
+      switch (side) {
+        case 48: return launch_tiledw<48>(ctx, t, s);
+        case 64: return launch_tiledw<64>(ctx, t, s);
+        case 96: return launch_tiledw<96>(ctx, t, s);
+        default: return launch_tiledw<128>(ctx, t, s);
+      }
+    }
     switch (side) {
       case 16: return launch_tiled<16>(ctx, t, s);
       case 32: return launch_tiled<32>(ctx, t, s);
@@ -995,6 +1082,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   size_t lds;
   int W;
   if (use_windowed(ctx, K)) {
+    if (!window_exact(a.c)) return window_unsupported();
     a.q = d_q;
     a.p = d_p;
     a.fp_iters = d_it;
@@ -1096,6 +1184,7 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   if (rc) return rc;
   if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
   if (n == 0) return RHMC_OK;
+  if (!window_exact(a.c)) return window_unsupported();  // integrate_win_kernel
   a.q = d_q;
   a.p = d_p;
   a.fp_iters = nullptr;
@@ -1295,6 +1384,7 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   size_t lds;
   int W;
   const bool win = use_windowed(ctx, K);
+  if (win && !window_exact(a.c)) return window_unsupported();
   if (win)
     pick_waves_win(ctx, K, &lds, &W);
   else if ((rc = pick_waves(ctx, K, &lds, &W)))

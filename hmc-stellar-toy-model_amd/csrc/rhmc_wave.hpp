@@ -135,11 +135,111 @@ __device__ __forceinline__ void inv_metric(double f, const LeanConsts& l, double
   ihxx = (u * fma(l.Bg2, u, l.inv_g1)) * l.inv_gxx;
 }
 
+// The two fixed-point loops of RHMC_single_step, evaluated SPEC iterations
+// per pass: the iterates of one pass depend on each other only through the
+// flux chain, so the reciprocals and the convergence tests of SPEC iterations
+// overlap instead of paying one dependent chain + one branch per iteration.
+// The state and iteration count returned are those of the first iteration
+// whose test stops the reference's loop (`while dp > delta and counter <
+// counter_max`, NaN stops); later speculative iterates are discarded.
+
+// p-loop (:528-535) on the flux momentum (dtaudq is zero on x, y): returns the
+// iteration count, `last` = the final |dp|.
+template <int SPEC>
+__device__ __forceinline__ int p_loop_spec(double& pf, double coef, double hdt, double delta,
+                                           int cmax, double& last) {
+  const double rho = pf;
+  int n = 0;
+  for (;;) {
+    double P[SPEC + 1], d[SPEC];
+    P[0] = pf;
+#pragma unroll
+    for (int k = 0; k < SPEC; ++k) {
+      P[k + 1] = rho - hdt * ((P[k] * P[k]) * coef / 2.0);
+      d[k] = fabs(P[k] - P[k + 1]);
+    }
+    bool stop = false;
+    double sel = P[SPEC], dsel = d[SPEC - 1];
+    int take = SPEC;
+#pragma unroll
+    for (int k = SPEC - 1; k >= 0; --k) {
+      if (!(d[k] > delta) || n + k + 1 >= cmax) {
+        stop = true;
+        take = k + 1;
+        sel = P[k + 1];
+        dsel = d[k];
+      }
+    }
+    pf = sel;
+    n += take;
+    if (stop) {
+      last = dsel;
+      return n;
+    }
+  }
+}
+
+// q-loop (:538-545): q_{n+1} = q_s + hdt (p/H(q_s) + p/H(q_n)).
+template <int SPEC>
+__device__ __forceinline__ int q_loop_spec(double& f, double& x, double& y, double pf, double px,
+                                           double py, double hdt, const LeanConsts& lc,
+                                           double delta, int cmax, double& last);
+
 // -H_ff'/H_ff^2 = (A/Bf)^2  (dtaudq's coefficient, :479)
 __device__ __forceinline__ double dtaudq_coef_lean(double f, const LeanConsts& l) {
   const double A = fma(f, l.inv_gff2, l.c0);
   const double t = A * rcp_nr(f + l.c0);
   return t * t;
+}
+
+template <int SPEC>
+__device__ __forceinline__ int q_loop_spec(double& f, double& x, double& y, double pf, double px,
+                                           double py, double hdt, const LeanConsts& lc,
+                                           double delta, int cmax, double& last) {
+  const double sf = f, sx = x, sy = y;
+  double ihff, ihxx;
+  inv_metric(sf, lc, ihff, ihxx);
+  const double af = pf * ihff, ax = px * ihxx, ay = py * ihxx;
+  int n = 0;
+  for (;;) {
+    double F[SPEC + 1], X[SPEC + 1], Y[SPEC + 1], d[SPEC];
+    F[0] = f;
+    X[0] = x;
+    Y[0] = y;
+#pragma unroll
+    for (int k = 0; k < SPEC; ++k) {
+      inv_metric(F[k], lc, ihff, ihxx);
+      F[k + 1] = sf + hdt * (af + pf * ihff);
+      X[k + 1] = sx + hdt * (ax + px * ihxx);
+      Y[k + 1] = sy + hdt * (ay + py * ihxx);
+      const double a0 = fabs(F[k] - F[k + 1]), a1 = fabs(X[k] - X[k + 1]),
+                   a2 = fabs(Y[k] - Y[k + 1]);
+      const double sum = a0 + a1 + a2;
+      d[k] = (sum != sum) ? sum : fmax(fmax(a0, a1), a2);  // np.max propagates NaN
+    }
+    bool stop = false;
+    double sf_ = F[SPEC], sx_ = X[SPEC], sy_ = Y[SPEC], dsel = d[SPEC - 1];
+    int take = SPEC;
+#pragma unroll
+    for (int k = SPEC - 1; k >= 0; --k) {
+      if (!(d[k] > delta) || n + k + 1 >= cmax) {
+        stop = true;
+        take = k + 1;
+        sf_ = F[k + 1];
+        sx_ = X[k + 1];
+        sy_ = Y[k + 1];
+        dsel = d[k];
+      }
+    }
+    f = sf_;
+    x = sx_;
+    y = sy_;
+    n += take;
+    if (stop) {
+      last = dsel;
+      return n;
+    }
+  }
 }
 
 // (H_ff'/H_ff + 2 H_xx'/H_xx)/2 with H_ff'/H_ff = -A/Bf^2 and

@@ -1,0 +1,117 @@
+// isa_bench.hip — fp64 VALU issue costs on gfx950 (tools only, not shipped).
+// Prints SIMD-cycles per wave64 instruction for independent FMA streams,
+// independent v_rcp_f64 streams, dependent FMA chains, and the accuracy of
+// raw v_rcp_f64 / one Newton step against IEEE 1/x.
+// build: hipcc --offload-arch=gfx950 -O3 -o tools/isa_bench tools/isa_bench.hip
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+template <int MODE>
+__global__ void thr(double* out, double seed, int iters) {
+  double a0 = seed + threadIdx.x * 1e-3, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
+         a5 = a0 + 5, a6 = a0 + 6, a7 = a0 + 7;
+  const double m = 0.9999999, c = 1e-7;
+  for (int i = 0; i < iters; ++i) {
+    if (MODE == 0) {  // 8 independent fma streams
+      a0 = fma(a0, m, c); a1 = fma(a1, m, c); a2 = fma(a2, m, c); a3 = fma(a3, m, c);
+      a4 = fma(a4, m, c); a5 = fma(a5, m, c); a6 = fma(a6, m, c); a7 = fma(a7, m, c);
+    } else if (MODE == 1) {  // 8 independent rcp streams
+      a0 = __builtin_amdgcn_rcp(a0); a1 = __builtin_amdgcn_rcp(a1);
+      a2 = __builtin_amdgcn_rcp(a2); a3 = __builtin_amdgcn_rcp(a3);
+      a4 = __builtin_amdgcn_rcp(a4); a5 = __builtin_amdgcn_rcp(a5);
+      a6 = __builtin_amdgcn_rcp(a6); a7 = __builtin_amdgcn_rcp(a7);
+    } else if (MODE == 2) {  // one dependent fma chain (latency)
+      a0 = fma(a0, m, c); a0 = fma(a0, m, c); a0 = fma(a0, m, c); a0 = fma(a0, m, c);
+      a0 = fma(a0, m, c); a0 = fma(a0, m, c); a0 = fma(a0, m, c); a0 = fma(a0, m, c);
+    } else if (MODE == 3) {  // two interleaved dependent chains
+      a0 = fma(a0, m, c); a1 = fma(a1, m, c); a0 = fma(a0, m, c); a1 = fma(a1, m, c);
+      a0 = fma(a0, m, c); a1 = fma(a1, m, c); a0 = fma(a0, m, c); a1 = fma(a1, m, c);
+    } else if (MODE == 4) {  // 8 independent v_mul_f64
+      a0 *= m; a1 *= m; a2 *= m; a3 *= m; a4 *= m; a5 *= m; a6 *= m; a7 *= m;
+    } else if (MODE == 5) {  // rcp mixed 1:6 with fma (pixel-loop ratio)
+      a0 = __builtin_amdgcn_rcp(a0); a1 = fma(a1, m, c); a2 = fma(a2, m, c); a3 = fma(a3, m, c);
+      a4 = fma(a4, m, c); a5 = fma(a5, m, c); a6 = fma(a6, m, c); a7 = fma(a7, m, c);
+    } else if (MODE == 6) {  // exp (ocml) x8 independent
+      a0 = exp(-a0); a1 = exp(-a1); a2 = exp(-a2); a3 = exp(-a3);
+      a4 = exp(-a4); a5 = exp(-a5); a6 = exp(-a6); a7 = exp(-a7);
+    }
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7;
+}
+
+__global__ void rcp_acc(const double* x, unsigned long long* stat, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double d = x[i];
+  const double ref = 1.0 / d;
+  const double r0 = __builtin_amdgcn_rcp(d);
+  const double r1 = fma(r0, fma(-d, r0, 1.0), r0);
+  auto ulp = [](double a, double b) {
+    long long x = __double_as_longlong(a) - __double_as_longlong(b);
+    return (unsigned long long)(x < 0 ? -x : x);
+  };
+  atomicMax(&stat[0], ulp(r0, ref));
+  atomicMax(&stat[1], ulp(r1, ref));
+  if (r1 != ref) atomicAdd(&stat[2], 1ull);
+}
+
+template <int MODE>
+float run(int blocks, int iters) {
+  double* out;
+  hipMalloc(&out, (size_t)blocks * 64 * 8);
+  hipEvent_t a, b;
+  hipEventCreate(&a);
+  hipEventCreate(&b);
+  thr<MODE><<<blocks, 64>>>(out, 1.5, 10);
+  hipEventRecord(a);
+  thr<MODE><<<blocks, 64>>>(out, 1.5, iters);
+  hipEventRecord(b);
+  hipEventSynchronize(b);
+  float ms;
+  hipEventElapsedTime(&ms, a, b);
+  hipFree(out);
+  return ms;
+}
+
+int main() {
+  hipDeviceProp_t prop;
+  hipGetDeviceProperties(&prop, 0);
+  const int simds = prop.multiProcessorCount * 4;
+  const double ghz = 2.4;
+  const char* names[] = {"fma x8 indep", "rcp x8 indep", "fma dep chain", "fma 2 chains",
+                         "mul x8 indep", "rcp:fma 1:7", "exp x8 indep"};
+  const int iters = 20000;
+  for (int wps : {1, 2, 4}) {
+    const int blocks = simds * wps;
+    float t[7];
+    t[0] = run<0>(blocks, iters);
+    t[1] = run<1>(blocks, iters);
+    t[2] = run<2>(blocks, iters);
+    t[3] = run<3>(blocks, iters);
+    t[4] = run<4>(blocks, iters);
+    t[5] = run<5>(blocks, iters);
+    t[6] = run<6>(blocks, iters / 20);
+    for (int m = 0; m < 7; ++m) {
+      const double ops = (double)wps * iters / (m == 6 ? 20 : 1) * 8;  // wave-ops per SIMD
+      printf("waves/SIMD %d  %-14s %8.3f ms  %6.2f cycles/wave-op @%.1fGHz\n", wps, names[m],
+             t[m], t[m] * 1e-3 * ghz * 1e9 / ops, ghz);
+    }
+  }
+  const int n = 1 << 24;
+  std::vector<double> hx(n);
+  for (int i = 0; i < n; ++i) hx[i] = 24.98 * std::pow(2.0, 14.0 * (double)i / n) * (1 + 1e-7 * (i % 977));
+  double* dx;
+  unsigned long long* st;
+  hipMalloc(&dx, n * 8);
+  hipMalloc(&st, 24);
+  hipMemset(st, 0, 24);
+  hipMemcpy(dx, hx.data(), n * 8, hipMemcpyHostToDevice);
+  rcp_acc<<<n / 256, 256>>>(dx, st, n);
+  unsigned long long hs[3];
+  hipMemcpy(hs, st, 24, hipMemcpyDeviceToHost);
+  printf("v_rcp_f64: max %llu ulp; + 1 Newton: max %llu ulp, %llu / %d differ from IEEE\n",
+         hs[0], hs[1], hs[2], n);
+  return 0;
+}
