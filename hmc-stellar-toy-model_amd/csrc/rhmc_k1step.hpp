@@ -1,0 +1,127 @@
+// rhmc_k1step.hpp — the step loop of RHMC_single_step (sampler_RHMC.py:522-566)
+// for one star, shared by the single-star kernels: every lane of a chain's
+// lane group holds the same (q, p) and runs the same scalar code; only the
+// gradient's pixel sum is spread over the group (the GRAD functor).
+//
+// The flux f changes only inside the q-loop, so every metric quantity a step
+// needs at its current f — 1/H_ff, H_xx's s, dtaudq's coefficient, the dphidq
+// metric term and the prior term — is computed once per distinct f
+// (FluxMetric) and reused by the gradient, the next p-loop and the q-loop's
+// q_tmp_s evaluation: three reciprocals per step plus one per q iteration,
+// instead of six plus one.
+#pragma once
+#include "rhmc.h"
+#include "rhmc_wave.hpp"
+
+namespace rhmc {
+
+// 1/d to within ~11 ulp (v_rcp_f64 is accurate to ~2^-24; one Newton step).
+__device__ __forceinline__ double rcp_nr1(double d) {
+  const double r = __builtin_amdgcn_rcp(d);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+
+struct FluxMetric {
+  double A;      // f/g_ff2 + (B/g0)/g_ff = 1/H_ff                       (:290)
+  double s;      // u/g1 + (B/g2) u^2, u = 1/max(f, f_low); H_xx = g_xx/s (:267-273)
+  double coef;   // -H_ff'/H_ff^2 = (A/(f + (B/g0)/g_ff))^2               (:479)
+  double mterm;  // (H_ff'/H_ff + 2 H_xx'/H_xx)/2                        (:459-463)
+  double prior;  // alpha/f (use_prior)                                    (:408-409)
+};
+
+__device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
+                                                  const LeanConsts& l) {
+  FluxMetric m;
+  m.A = fma(f, l.inv_gff2, l.c0);
+  const double ib = rcp_nr(f + l.c0);
+  const double t = m.A * ib;
+  m.coef = t * t;
+  const bool low = f < l.f_low;
+  const double fl = low ? l.f_low : f;
+  const double u = rcp_nr(fl);
+  m.s = u * fma(l.Bg2, u, l.inv_g1);
+  const double t2 = low ? 0.0 : (u * u) * fma(2.0 * l.Bg2, u, l.inv_g1) * rcp_nr(m.s);
+  const double t1 = -m.A * (ib * ib);
+  m.mterm = (t1 + 2.0 * t2) / 2.0;
+  m.prior = c.use_prior ? c.alpha * (low ? rcp_nr(f) : u) : 0.0;
+  return m;
+}
+
+// n_steps steps on (f, x, y, pf, px, py).  grad(f, x, y, gf, gx, gy) returns
+// the pixel part of dphidq: gf = -sum psf (D/L - 1), gx, gy (:404-406).
+template <class GRAD>
+__device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double& pf,
+                                         double& px, double& py, int n_steps, double edge,
+                                         const Consts& c, const LeanConsts& lc, GRAD grad,
+                                         int& it_p, int& it_q, unsigned& st) {
+  const double hdt = c.hdt;
+  FluxMetric fm = flux_metric(f, c, lc);
+  for (int s = 0;; ++s) {
+    double gf, gx, gy;
+    grad(f, x, y, gf, gx, gy);
+    if (c.use_prior) gf += fm.prior;               // :408-409
+    gf += fm.mterm;                                // :459-463
+    if (s > 0) {
+      pf = pf - hdt * gf;                          // :551
+      px = px - hdt * gx;
+      py = py - hdt * gy;
+      if (f < c.f_lim) {                           // :554-564
+        pf = -pf;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+      if (x < 0.0 || x > edge) {
+        px = -px;
+        st |= RHMC_STATUS_REFLECT_XY;
+      }
+      if (y < 0.0 || y > edge) {
+        py = -py;
+        st |= RHMC_STATUS_REFLECT_XY;
+      }
+    }
+    if (s == n_steps) break;
+    pf = pf - hdt * gf;                            // :525
+    px = px - hdt * gx;
+    py = py - hdt * gy;
+    {                                              // :528-535 (dtaudq is 0 on x, y)
+      const double rho = pf, hc = hdt * (fm.coef * 0.5);
+      double dp;
+      int n = 0;
+      do {
+        const double pp = fma(-hc, pf * pf, rho);
+        dp = fabs(pf - pp);
+        pf = pp;
+        ++n;
+      } while (dp > c.delta && n < c.counter_max);
+      it_p += n;
+      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
+    }
+    {                                              // :538-545
+      const double sf = f, sx = x, sy = y;
+      const double af = pf * fm.A, ax = px * (fm.s * lc.inv_gxx), ay = py * (fm.s * lc.inv_gxx);
+      double dq;
+      int n = 0;
+      do {
+        const double ihff = fma(f, lc.inv_gff2, lc.c0);
+        const double fl = (f < lc.f_low) ? lc.f_low : f;
+        const double u = rcp_nr1(fl);
+        const double ihxx = (u * fma(lc.Bg2, u, lc.inv_g1)) * lc.inv_gxx;
+        const double nf = sf + hdt * (af + pf * ihff);
+        const double nx = sx + hdt * (ax + px * ihxx);
+        const double ny = sy + hdt * (ay + py * ihxx);
+        const double a0 = fabs(f - nf), a1 = fabs(x - nx), a2 = fabs(y - ny);
+        const double sum = a0 + a1 + a2;
+        dq = (sum != sum) ? sum : fmax(fmax(a0, a1), a2);  // np.max propagates NaN
+        f = nf;
+        x = nx;
+        y = ny;
+        ++n;
+      } while (dq > c.delta && n < c.counter_max);
+      it_q += n;
+      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
+    }
+    fm = flux_metric(f, c, lc);
+    pf = pf - hdt * ((pf * pf) * fm.coef / 2.0);   // :548
+  }
+}
+
+}  // namespace rhmc

@@ -745,11 +745,12 @@ int window_unsupported() {
               "that needs the windowed kernels (K > 16 or image larger than LDS)");
 }
 
-// RHMC_KERNEL=tiledw forces the windowed single-star kernel, "tiled2"/"tiled1"
+// RHMC_KERNEL=tiledw / tiledw32 force the windowed single-star kernel (16 / 32
+// lanes per chain), "tiled2"/"tiled1"
 // and the generic-LPC names below force full-image kernels.
 bool force_full_image_k1() {
   const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strcmp(e, "tiledw") != 0 && std::strncmp(e, "tiled", 5) == 0;
+  return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiled", 5) == 0;
 }
 
 // RHMC_KERNEL=tiled4 / tiled4w1 / tiledg32 / tiledg64: the generic-LPC kernel
@@ -964,9 +965,9 @@ int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
-template <int IMG>
-int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  using TL = TiledW<IMG>;
+template <int IMG, int LPC>
+int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  using TL = TiledW<IMG, LPC>;
   int W = 4;
   size_t lds = TL::lds_doubles(W) * sizeof(double);
   while (lds > (size_t)ctx->max_lds && W > 1) {
@@ -974,11 +975,20 @@ int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
     lds = TL::lds_doubles(W) * sizeof(double);
   }
   if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
-  const int64_t waves = (a.n_chains + 1) / 2;
+  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL(leapfrog_k1_tiledw<IMG>, grid, block, lds, s, a);
+  hipLaunchKernelGGL((leapfrog_k1_tiledw<IMG, LPC>), grid, block, lds, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
+}
+
+// Lanes per chain of the windowed single-star kernel: 16 (4 chains per wave,
+// the default) or 32 (RHMC_KERNEL=tiledw32).
+template <int IMG>
+int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  if (e && std::strcmp(e, "tiledw32") == 0) return launch_tiledw_lpc<IMG, 32>(ctx, a, s);
+  return launch_tiledw_lpc<IMG, 16>(ctx, a, s);
 }
 
 // V (and optionally T) of n chains on device buffers, async on `s`.

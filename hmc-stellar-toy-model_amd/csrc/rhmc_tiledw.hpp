@@ -1,5 +1,5 @@
 // rhmc_tiledw.hpp — single-star leapfrog on a 32 x 32 pixel window per chain,
-// two chains per wave64 (32 lanes each).
+// 64/LPC chains per wave64 (LPC = 32 or 16 lanes per chain).
 //
 // Every pixel of the reference's dphidq sum (sampler_RHMC.py:365-425) carries
 // a factor PSF_ij; a pixel centre >= 15.5 px from the star has
@@ -13,11 +13,13 @@
 // bound above holds (window_exact), else the full-image tiled kernels.
 //
 // Layout: D row-major in LDS with pitch P = IMG + 1 (P % 4 == 1).  Lane (a, b)
-// of a half-wave (a = m >> 3 in 0..3, b = m & 7) owns window rows 8a .. 8a+7
-// and the strided window columns b, b+8, b+16, b+24; the 32 addresses of one
-// read are then (8a P + b) mod 32 distinct doubles — conflict-free — while the
-// row/column product structure that separability needs is kept.
+// of a chain's group (a = m / GC in 0..3, b = m % GC, GC = LPC/4) owns window
+// rows 8a .. 8a+7 and the strided window columns b, b+GC, b+2GC, ...; the
+// addresses of one read are then (8a P + b) mod 32 distinct doubles within a
+// group — conflict-free — while the row/column product structure that
+// separability needs is kept.
 #pragma once
+#include "rhmc_k1step.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
 #include "rhmc_wave.hpp"
@@ -25,12 +27,16 @@
 
 namespace rhmc {
 
-template <int IMG>
+template <int IMG, int LPC>
 struct TiledW {
-  static constexpr int P = IMG + 1;    // LDS row pitch
-  static constexpr int TR = 8;         // window rows per lane
-  static constexpr int TC = 4;         // window columns per lane (stride 8)
-  static constexpr int TAB = 2 * 128;  // per wave: 2 chains x 64 (value, offset) pairs
+  static_assert(LPC == 16 || LPC == 32, "LPC in {16, 32}");
+  static constexpr int CPW = kWave / LPC;  // chains per wave
+  static constexpr int GC = LPC / 4;       // lane grid columns (4 lane rows)
+  static constexpr int P = IMG + 1;        // LDS row pitch
+  static constexpr int TR = 8;             // window rows per lane
+  static constexpr int TC = kWin / GC;     // window columns per lane (stride GC)
+  static constexpr int NE = 2 * kWin / LPC;  // factor entries per lane
+  static constexpr int TAB = CPW * 128;    // per wave: 64 (value, offset) pairs per chain
   static_assert(IMG >= kWin && IMG % 4 == 0, "window inside the image, P % 4 == 1");
 
   static __host__ __device__ constexpr size_t lds_doubles(int waves) {
@@ -41,23 +47,35 @@ struct TiledW {
     return o < 0 ? 0 : (o > IMG - kWin ? IMG - kWin : o);
   }
 
-  // dphidq of the half-wave's chain (every lane of the half gets it).
+  static __device__ __forceinline__ double group_sum(double v) {
+    v += dpp_move<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_move<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_move<0x141>(v);  // row_half_mirror
+    v += dpp_move<0x140>(v);  // row_mirror: 16-lane sums
+    if constexpr (LPC == 32) v = swap_add<false>(v);  // v_permlane16_swap
+    return v;
+  }
+
+  // Pixel part of the group's chain's dphidq (every lane of the group gets
+  // it); the metric and prior terms are added by k1_steps.
   static __device__ __forceinline__ void gradient(const double* __restrict__ sD, double* tab,
                                                   double f, double x, double y, const Consts& c,
                                                   const LeanConsts& lc, double& gf, double& gx,
                                                   double& gy) {
     const int lane = lane_id();
-    const int h = lane >> 5, m = lane & 31;
-    const int a = m >> 3, b = m & 7;
+    const int h = lane / LPC, m = lane % LPC;
+    const int a = m / GC, b = m % GC;
     const int r0 = origin(x), c0 = origin(y);
     double* t = tab + h * 128;  // rows [32][2], cols [32][2]
-    {
-      const double vr = ((r0 + m) + 0.5) - x;
-      t[2 * m] = exp(-(vr * vr) * lc.inv_two_sig2);
-      t[2 * m + 1] = ((double)(r0 + m) - x) + 0.5;
-      const double vc = ((c0 + m) + 0.5) - y;
-      t[64 + 2 * m] = exp(-(vc * vc) * lc.inv_two_sig2) * lc.inv_norm;
-      t[64 + 2 * m + 1] = ((double)(c0 + m) - y) + 0.5;
+#pragma unroll
+    for (int n = 0; n < kWin / LPC; ++n) {
+      const int e = n * LPC + m;
+      const double vr = ((r0 + e) + 0.5) - x;
+      t[2 * e] = exp(-(vr * vr) * lc.inv_two_sig2);
+      t[2 * e + 1] = ((double)(r0 + e) - x) + 0.5;
+      const double vc = ((c0 + e) + 0.5) - y;
+      t[64 + 2 * e] = exp(-(vc * vc) * lc.inv_two_sig2) * lc.inv_norm;
+      t[64 + 2 * e + 1] = ((double)(c0 + e) - y) + 0.5;
     }
     wave_lds_sync();
     double ex[TR], dx[TR], ey[TC], dy[TC];
@@ -68,8 +86,8 @@ struct TiledW {
     }
 #pragma unroll
     for (int k = 0; k < TC; ++k) {
-      ey[k] = t[64 + 2 * (b + 8 * k)];
-      dy[k] = t[64 + 2 * (b + 8 * k) + 1];
+      ey[k] = t[64 + 2 * (b + GC * k)];
+      dy[k] = t[64 + 2 * (b + GC * k) + 1];
     }
     wave_lds_sync();
 
@@ -86,7 +104,7 @@ struct TiledW {
 #pragma unroll
     for (int pp = 0; pp < TR * TC; pp += 2) {
       const int i1 = pp / TC, j1 = pp % TC, i2 = (pp + 1) / TC, j2 = (pp + 1) % TC;
-      const double d1 = sDl[i1 * P + 8 * j1], d2 = sDl[i2 * P + 8 * j2];
+      const double d1 = sDl[i1 * P + GC * j1], d2 = sDl[i2 * P + GC * j2];
       const double l1 = fma(fex[i1], ey[j1], c.B), l2 = fma(fex[i2], ey[j2], c.B);  // :373-376
       const double L = l1 * l2;
       double r = __builtin_amdgcn_rcp(L);
@@ -106,21 +124,19 @@ struct TiledW {
     }
 #pragma unroll
     for (int k = 0; k < TC; ++k) a2 = fma(ey[k] * C[k], dy[k], a2);
-    const double s0 = half_sum_dpp(a0);
-    const double s1 = half_sum_dpp(a1);
-    const double s2 = half_sum_dpp(a2);
+    const double s0 = group_sum(a0);
+    const double s1 = group_sum(a1);
+    const double s2 = group_sum(a2);
     gf = -s0;                                          // :404
     gx = -s1 * f * lc.inv_var;                         // :405
     gy = -s2 * f * lc.inv_var;                         // :406
-    if (c.use_prior) gf += c.alpha * rcp_nr(f);        // :408-409
-    gf += metric_flux_term_lean(f, lc);                // :459-463
   }
 };
 
-template <int IMG>
+template <int IMG, int LPC>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_k1_tiledw(LeapArgsK1 a) {
-  using TL = TiledW<IMG>;
+  using TL = TiledW<IMG, LPC>;
   extern __shared__ double lds[];
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
@@ -130,86 +146,26 @@ leapfrog_k1_tiledw(LeapArgsK1 a) {
   }
   __syncthreads();
   const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
-  if (2 * wave >= a.n_chains) return;
+  if (TL::CPW * wave >= a.n_chains) return;
   const int lane = lane_id();
-  const int h = lane >> 5;
-  const int64_t chain = 2 * wave + h;
-  const bool real = chain < a.n_chains;            // odd count: the last half mirrors
-  const int64_t base = (real ? chain : 2 * wave) * 3;
+  const int h = lane / LPC;
+  const int64_t chain = TL::CPW * wave + h;
+  const bool real = chain < a.n_chains;            // ragged tail: mirror the wave's first chain
+  const int64_t base = (real ? chain : TL::CPW * wave) * 3;
   double* tab = lds + (size_t)IMG * TL::P + (threadIdx.x / kWave) * TL::TAB;
 
   double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
   double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
-  const double hdt = c.hdt;
   const LeanConsts lc = lean_consts(c);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
+  k1_steps(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
+           [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
+             TL::gradient(lds, tab, f_, x_, y_, c, lc, gf, gx, gy);
+           },
+           it_p, it_q, st);
 
-  for (int s = 0;; ++s) {
-    double gf, gx, gy;
-    TL::gradient(lds, tab, f, x, y, c, lc, gf, gx, gy);
-    if (s > 0) {
-      pf = pf - hdt * gf;                          // :551
-      px = px - hdt * gx;
-      py = py - hdt * gy;
-      if (f < c.f_lim) {                           // :554-564
-        pf = -pf;
-        st |= RHMC_STATUS_REFLECT_F;
-      }
-      if (x < 0.0 || x > (double)(IMG - 1)) {
-        px = -px;
-        st |= RHMC_STATUS_REFLECT_XY;
-      }
-      if (y < 0.0 || y > (double)(IMG - 1)) {
-        py = -py;
-        st |= RHMC_STATUS_REFLECT_XY;
-      }
-    }
-    if (s == a.n_steps) break;
-    pf = pf - hdt * gf;                            // :525
-    px = px - hdt * gx;
-    py = py - hdt * gy;
-    {                                              // :528-535
-      const double coef = dtaudq_coef_lean(f, lc);
-      const double rho = pf;
-      double dp;
-      int n = 0;
-      do {
-        const double pp = rho - hdt * ((pf * pf) * coef / 2.0);
-        dp = fabs(pf - pp);
-        pf = pp;
-        ++n;
-      } while (dp > c.delta && n < c.counter_max);
-      it_p += n;
-      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
-    }
-    {                                              // :538-545
-      const double sf = f, sx = x, sy = y;
-      double ihff, ihxx;
-      inv_metric(sf, lc, ihff, ihxx);
-      const double af = pf * ihff, ax = px * ihxx, ay = py * ihxx;
-      double dq;
-      int n = 0;
-      do {
-        inv_metric(f, lc, ihff, ihxx);
-        const double nf = sf + hdt * (af + pf * ihff);
-        const double nx = sx + hdt * (ax + px * ihxx);
-        const double ny = sy + hdt * (ay + py * ihxx);
-        const double a0 = fabs(f - nf), a1 = fabs(x - nx), a2 = fabs(y - ny);
-        const double sum = a0 + a1 + a2;
-        dq = (sum != sum) ? sum : fmax(fmax(a0, a1), a2);
-        f = nf;
-        x = nx;
-        y = ny;
-        ++n;
-      } while (dq > c.delta && n < c.counter_max);
-      it_q += n;
-      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
-    }
-    pf = pf - hdt * ((pf * pf) * dtaudq_coef_lean(f, lc) / 2.0);   // :548
-  }
-
-  if ((lane & 31) == 0 && real) {
+  if ((lane % LPC) == 0 && real) {
     if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
           isfinite(py)))
       st |= RHMC_STATUS_NONFINITE;
