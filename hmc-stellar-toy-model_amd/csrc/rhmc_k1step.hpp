@@ -49,16 +49,29 @@ __device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
 
 // n_steps steps on (f, x, y, pf, px, py).  grad(f, x, y, gf, gx, gy) returns
 // the pixel part of dphidq: gf = -sum psf (D/L - 1), gx, gy (:404-406).
-template <class GRAD>
+// PROF (tools only): prof[0] += cycles in grad, prof[1] += cycles elsewhere.
+template <bool PROF = false, class GRAD>
 __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double& pf,
                                          double& px, double& py, int n_steps, double edge,
                                          const Consts& c, const LeanConsts& lc, GRAD grad,
-                                         int& it_p, int& it_q, unsigned& st) {
+                                         int& it_p, int& it_q, unsigned& st,
+                                         long long* prof = nullptr) {
   const double hdt = c.hdt;
   FluxMetric fm = flux_metric(f, c, lc);
+  long long t0 = 0;
   for (int s = 0;; ++s) {
     double gf, gx, gy;
+    if constexpr (PROF) {
+      const long long t1 = clock64();
+      if (s > 0) prof[1] += t1 - t0;
+      t0 = t1;
+    }
     grad(f, x, y, gf, gx, gy);
+    if constexpr (PROF) {
+      const long long t1 = clock64();
+      prof[0] += t1 - t0;
+      t0 = t1;
+    }
     if (c.use_prior) gf += fm.prior;               // :408-409
     gf += fm.mterm;                                // :459-463
     if (s > 0) {
@@ -96,28 +109,30 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
     }
     {                                              // :538-545
-      const double sf = f, sx = x, sy = y;
-      const double af = pf * fm.A, ax = px * (fm.s * lc.inv_gxx), ay = py * (fm.s * lc.inv_gxx);
-      double dq;
+      // q_{n+1} = q_s + hdt (p/H(q_s) + p/H(q_n)) with 1/H_ff(f) = f/g_ff2 + c0
+      // and 1/H_xx(f) = g(f)/g_xx, g = u/g1 + (B/g2) u^2: affine in f and g.
+      const double ihxx_s = fm.s * lc.inv_gxx;
+      const double bf = hdt * (pf * lc.inv_gff2), cf = f + hdt * (pf * fm.A + pf * lc.c0);
+      const double bx = hdt * (px * lc.inv_gxx), cx = x + hdt * (px * ihxx_s);
+      const double by = hdt * (py * lc.inv_gxx), cy = y + hdt * (py * ihxx_s);
+      bool more;
       int n = 0;
       do {
-        const double ihff = fma(f, lc.inv_gff2, lc.c0);
         const double fl = (f < lc.f_low) ? lc.f_low : f;
         const double u = rcp_nr1(fl);
-        const double ihxx = (u * fma(lc.Bg2, u, lc.inv_g1)) * lc.inv_gxx;
-        const double nf = sf + hdt * (af + pf * ihff);
-        const double nx = sx + hdt * (ax + px * ihxx);
-        const double ny = sy + hdt * (ay + py * ihxx);
+        const double g = u * fma(lc.Bg2, u, lc.inv_g1);
+        const double nf = fma(bf, f, cf), nx = fma(bx, g, cx), ny = fma(by, g, cy);
         const double a0 = fabs(f - nf), a1 = fabs(x - nx), a2 = fabs(y - ny);
         const double sum = a0 + a1 + a2;
-        dq = (sum != sum) ? sum : fmax(fmax(a0, a1), a2);  // np.max propagates NaN
+        // dq = np.max(...) > delta, NaN stops the loop
+        more = (fmax(fmax(a0, a1), a2) > c.delta) && (sum == sum);
         f = nf;
         x = nx;
         y = ny;
         ++n;
-      } while (dq > c.delta && n < c.counter_max);
+      } while (more && n < c.counter_max);
       it_q += n;
-      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
+      if (more) st |= RHMC_STATUS_QLOOP_CAP;
     }
     fm = flux_metric(f, c, lc);
     pf = pf - hdt * ((pf * pf) * fm.coef / 2.0);   // :548

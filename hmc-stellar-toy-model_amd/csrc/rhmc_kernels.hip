@@ -965,7 +965,7 @@ int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
-template <int IMG, int LPC>
+template <int IMG, int LPC, bool PROF = false>
 int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   using TL = TiledW<IMG, LPC>;
   int W = 4;
@@ -975,9 +975,13 @@ int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
     lds = TL::lds_doubles(W) * sizeof(double);
   }
   if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+  if (const char* pad = std::getenv("RHMC_LDS_MIN")) {  // experiment: cap workgroups per CU
+    const size_t want = (size_t)std::atol(pad);
+    if (want > lds && want <= (size_t)ctx->max_lds) lds = want;
+  }
   const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_k1_tiledw<IMG, LPC>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((leapfrog_k1_tiledw<IMG, LPC, PROF>), grid, block, lds, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -988,6 +992,8 @@ template <int IMG>
 int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   const char* e = std::getenv("RHMC_KERNEL");
   if (e && std::strcmp(e, "tiledw32") == 0) return launch_tiledw_lpc<IMG, 32>(ctx, a, s);
+  if (e && std::strcmp(e, "profw16") == 0) return launch_tiledw_lpc<IMG, 16, true>(ctx, a, s);
+  if (e && std::strcmp(e, "profw32") == 0) return launch_tiledw_lpc<IMG, 32, true>(ctx, a, s);
   return launch_tiledw_lpc<IMG, 16>(ctx, a, s);
 }
 

@@ -19,6 +19,7 @@
 // group — conflict-free — while the row/column product structure that
 // separability needs is kept.
 #pragma once
+#include "rhmc_exp.hpp"
 #include "rhmc_k1step.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
@@ -39,8 +40,11 @@ struct TiledW {
   static constexpr int TAB = CPW * 128;    // per wave: 64 (value, offset) pairs per chain
   static_assert(IMG >= kWin && IMG % 4 == 0, "window inside the image, P % 4 == 1");
 
+  // LDS: D [IMG][P], the exp table, per-wave factor tables.
+  static constexpr int EXP_OFF = IMG * P;
+  static constexpr int TAB_OFF = IMG * P + kExpTab;
   static __host__ __device__ constexpr size_t lds_doubles(int waves) {
-    return (size_t)IMG * P + (size_t)waves * TAB;
+    return (size_t)TAB_OFF + (size_t)waves * TAB;
   }
   static __device__ __forceinline__ int origin(double v) {
     const int o = win_base(v);
@@ -71,10 +75,10 @@ struct TiledW {
     for (int n = 0; n < kWin / LPC; ++n) {
       const int e = n * LPC + m;
       const double vr = ((r0 + e) + 0.5) - x;
-      t[2 * e] = exp(-(vr * vr) * lc.inv_two_sig2);
+      t[2 * e] = exp_neg(-(vr * vr) * lc.inv_two_sig2, sD + EXP_OFF);
       t[2 * e + 1] = ((double)(r0 + e) - x) + 0.5;
       const double vc = ((c0 + e) + 0.5) - y;
-      t[64 + 2 * e] = exp(-(vc * vc) * lc.inv_two_sig2) * lc.inv_norm;
+      t[64 + 2 * e] = exp_neg(-(vc * vc) * lc.inv_two_sig2, sD + EXP_OFF) * lc.inv_norm;
       t[64 + 2 * e + 1] = ((double)(c0 + e) - y) + 0.5;
     }
     wave_lds_sync();
@@ -95,14 +99,9 @@ struct TiledW {
     const double* sDl = sD + (r0 + 8 * a) * P + c0 + b;
     double fex[TR], R[TR], C[TC];
 #pragma unroll
-    for (int k = 0; k < TR; ++k) {
-      fex[k] = f * ex[k];
-      R[k] = 0.0;
-    }
+    for (int k = 0; k < TR; ++k) fex[k] = f * ex[k];
 #pragma unroll
-    for (int k = 0; k < TC; ++k) C[k] = 0.0;
-#pragma unroll
-    for (int pp = 0; pp < TR * TC; pp += 2) {
+    for (int pp = 0; pp < TR * TC; pp += 2) {  // row-major pairs (i, j), (i, j + 1)
       const int i1 = pp / TC, j1 = pp % TC, i2 = (pp + 1) / TC, j2 = (pp + 1) % TC;
       const double d1 = sDl[i1 * P + GC * j1], d2 = sDl[i2 * P + GC * j2];
       const double l1 = fma(fex[i1], ey[j1], c.B), l2 = fma(fex[i2], ey[j2], c.B);  // :373-376
@@ -110,10 +109,10 @@ struct TiledW {
       double r = __builtin_amdgcn_rcp(L);
       r = fma(r, fma(-L, r, 1.0), r);
       const double s1 = fma(d1, l2 * r, -1.0), s2 = fma(d2, l1 * r, -1.0);  // D/Lambda - 1 (:379)
-      R[i1] = fma(ey[j1], s1, R[i1]);
-      C[j1] = fma(ex[i1], s1, C[j1]);
+      R[i1] = (j1 == 0) ? ey[j1] * s1 : fma(ey[j1], s1, R[i1]);
+      C[j1] = (i1 == 0) ? ex[i1] * s1 : fma(ex[i1], s1, C[j1]);
       R[i2] = fma(ey[j2], s2, R[i2]);
-      C[j2] = fma(ex[i2], s2, C[j2]);
+      C[j2] = (i2 == 0) ? ex[i2] * s2 : fma(ex[i2], s2, C[j2]);
     }
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
@@ -133,7 +132,8 @@ struct TiledW {
   }
 };
 
-template <int IMG, int LPC>
+// PROF (tools only): fp_iters[c] = (gradient, rest) cycles per step.
+template <int IMG, int LPC, bool PROF = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_k1_tiledw(LeapArgsK1 a) {
   using TL = TiledW<IMG, LPC>;
@@ -144,6 +144,7 @@ leapfrog_k1_tiledw(LeapArgsK1 a) {
     const int r = e / IMG, cc = e - (e / IMG) * IMG;
     lds[r * TL::P + cc] = a.D[e];
   }
+  exp_tab_fill(lds + TL::EXP_OFF);
   __syncthreads();
   const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (TL::CPW * wave >= a.n_chains) return;
@@ -152,18 +153,24 @@ leapfrog_k1_tiledw(LeapArgsK1 a) {
   const int64_t chain = TL::CPW * wave + h;
   const bool real = chain < a.n_chains;            // ragged tail: mirror the wave's first chain
   const int64_t base = (real ? chain : TL::CPW * wave) * 3;
-  double* tab = lds + (size_t)IMG * TL::P + (threadIdx.x / kWave) * TL::TAB;
+  double* tab = lds + TL::TAB_OFF + (threadIdx.x / kWave) * TL::TAB;
 
   double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
   double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
   const LeanConsts lc = lean_consts(c);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  k1_steps(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
-           [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
-             TL::gradient(lds, tab, f_, x_, y_, c, lc, gf, gx, gy);
-           },
-           it_p, it_q, st);
+  long long prof[2] = {0, 0};
+  k1_steps<PROF>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
+                 [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
+                   TL::gradient(lds, tab, f_, x_, y_, c, lc, gf, gx, gy);
+                 },
+                 it_p, it_q, st, prof);
+  if constexpr (PROF) {
+    const int ns = a.n_steps > 0 ? a.n_steps : 1;
+    it_p = (int)(prof[0] / ns);
+    it_q = (int)(prof[1] / ns);
+  }
 
   if ((lane % LPC) == 0 && real) {
     if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&

@@ -8,6 +8,8 @@
 #include <cstdio>
 #include <vector>
 
+#include "../hmc-stellar-toy-model_amd/csrc/rhmc_exp.hpp"
+
 template <int MODE>
 __global__ void thr(double* out, double seed, int iters) {
   double a0 = seed + threadIdx.x * 1e-3, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4,
@@ -75,6 +77,32 @@ float run(int blocks, int iters) {
   return ms;
 }
 
+__global__ void exp_acc(unsigned long long* stat, int n, double lo) {
+  __shared__ double tab[rhmc::kExpTab];
+  rhmc::exp_tab_fill(tab);
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double t = lo * ((double)i / n) * (1.0 + 1e-9 * (i % 1013));
+  const double a = rhmc::exp_neg(t, tab), b = exp(t);
+  long long d = __double_as_longlong(a) - __double_as_longlong(b);
+  d = d < 0 ? -d : d;
+  atomicMax(&stat[0], (unsigned long long)d);
+  if (d) atomicAdd(&stat[1], 1ull);
+}
+
+__global__ void exp_thr(double* out, double seed, int iters) {
+  __shared__ double tab[rhmc::kExpTab];
+  rhmc::exp_tab_fill(tab);
+  __syncthreads();
+  double a0 = -(seed + threadIdx.x * 1e-3), a1 = a0 - 1, a2 = a0 - 2, a3 = a0 - 3;
+  for (int i = 0; i < iters; ++i) {
+    a0 = -rhmc::exp_neg(a0, tab); a1 = -rhmc::exp_neg(a1, tab);
+    a2 = -rhmc::exp_neg(a2, tab); a3 = -rhmc::exp_neg(a3, tab);
+  }
+  out[blockIdx.x * blockDim.x + threadIdx.x] = a0 + a1 + a2 + a3;
+}
+
 int main() {
   hipDeviceProp_t prop;
   hipGetDeviceProperties(&prop, 0);
@@ -113,5 +141,30 @@ int main() {
   hipMemcpy(hs, st, 24, hipMemcpyDeviceToHost);
   printf("v_rcp_f64: max %llu ulp; + 1 Newton: max %llu ulp, %llu / %d differ from IEEE\n",
          hs[0], hs[1], hs[2], n);
+  {
+    unsigned long long* es;
+    hipMalloc(&es, 16);
+    for (double lo : {-30.0, -745.0, -1500.0}) {
+      hipMemset(es, 0, 16);
+      exp_acc<<<n / 256, 256>>>(es, n, lo);
+      unsigned long long he[2];
+      hipMemcpy(he, es, 16, hipMemcpyDeviceToHost);
+      printf("exp_neg vs exp on [%g, 0]: max %llu ulp, %llu / %d differ\n", lo, he[0], he[1], n);
+    }
+    double* out;
+    hipMalloc(&out, (size_t)simds * 4 * 64 * 8);
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    exp_thr<<<simds * 4, 64>>>(out, 1.5, 10);
+    hipEventRecord(a);
+    exp_thr<<<simds * 4, 64>>>(out, 1.5, 1000);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms;
+    hipEventElapsedTime(&ms, a, b);
+    printf("waves/SIMD 4  exp_neg x4 dep   %8.3f ms  %6.2f cycles/wave-op @2.4GHz\n", ms,
+           ms * 1e-3 * 2.4e9 / (4.0 * 1000 * 4));
+  }
   return 0;
 }

@@ -21,6 +21,10 @@ for _ in range(2):
 torch.cuda.synchronize()
 a = it.cpu().numpy().astype(float)
 b = st.cpu().numpy().astype(float)
-tot = a[:, 0] + a[:, 1] + b
-print("%s n=%d cycles/step: table %.0f  pixel+reduce %.0f  loops %.0f  total %.0f" % (
-    os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), b.mean(), tot.mean()))
+if os.environ.get("RHMC_KERNEL", "").startswith("profw"):
+    print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
+        os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), a.sum(1).mean()))
+else:
+    tot = a[:, 0] + a[:, 1] + b
+    print("%s n=%d cycles/step: table %.0f  pixel+reduce %.0f  loops %.0f  total %.0f" % (
+        os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), b.mean(), tot.mean()))
