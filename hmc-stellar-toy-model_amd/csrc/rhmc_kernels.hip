@@ -31,7 +31,6 @@
 #include "rhmc_mh.hpp"
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
-#include "rhmc_tiledg.hpp"
 #include "rhmc_tiledk.hpp"
 #include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
@@ -753,20 +752,6 @@ bool force_full_image_k1() {
   return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiled", 5) == 0;
 }
 
-// RHMC_KERNEL=tiled4 / tiled4w1 / tiledg32 / tiledg64: the generic-LPC kernel
-// with 16 (2 or 1 waves/EU budget), 32, 64 lanes per chain; 0 = not selected.
-int tiledg_lanes() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  if (!e) return 0;
-  if (std::strcmp(e, "tiled4") == 0) return 16;
-  if (std::strcmp(e, "tiled4w1") == 0) return 17;
-  if (std::strcmp(e, "tiledg32") == 0) return 32;
-  if (std::strcmp(e, "tiledg64") == 0) return 64;
-  if (std::strcmp(e, "prof16") == 0) return 116;   // phase-timing builds (tools only)
-  if (std::strcmp(e, "prof32") == 0) return 132;
-  return 0;
-}
-
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
 constexpr int kMaxK = 64;          // windowed kernel: lanes = stars
 
@@ -926,32 +911,8 @@ int launch_tiled2(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
-// Generic-LPC single-star kernel (rhmc_tiledg.hpp).
-template <int IMG, int LPC, int WPE, bool PROF = false>
-int launch_tiledg(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  using TL = TiledG<IMG, LPC>;
-  int W = 4;
-  size_t lds = TL::lds_doubles(W) * sizeof(double);
-  while (lds > (size_t)ctx->max_lds && W > 1) {
-    W >>= 1;
-    lds = TL::lds_doubles(W) * sizeof(double);
-  }
-  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
-  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_k1_tiledg<IMG, LPC, WPE, PROF>), grid, block, lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
-}
-
 template <int IMG>
 int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  const int lpc = tiledg_lanes();
-  if (lpc == 16) return launch_tiledg<IMG, 16, 2>(ctx, a, s);
-  if (lpc == 17) return launch_tiledg<IMG, 16, 1>(ctx, a, s);
-  if (lpc == 32) return launch_tiledg<IMG, 32, 2>(ctx, a, s);
-  if (lpc == 64) return launch_tiledg<IMG, 64, 2>(ctx, a, s);
-  if (lpc == 116) return launch_tiledg<IMG, 16, 2, true>(ctx, a, s);
-  if (lpc == 132) return launch_tiledg<IMG, 32, 2, true>(ctx, a, s);
   if (use_tiled2()) return launch_tiled2<IMG>(ctx, a, s);
   int W = 4;
   size_t lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);

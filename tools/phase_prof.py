@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-phase cycle split of the single-star kernel (RHMC_KERNEL=prof16|prof32):
+"""Per-phase cycle split of the single-star kernel (RHMC_KERNEL=profw16|profw32):
 table build, pixel loop + reductions, fixed-point loops; cycles per step per wave."""
 import os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hmc-stellar-toy-model_amd"))
