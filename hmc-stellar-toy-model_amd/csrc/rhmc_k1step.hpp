@@ -15,6 +15,16 @@
 
 namespace rhmc {
 
+// Fixed-point iterations evaluated per pass (one branch per pass).
+#ifndef RHMC_SPEC_P
+#define RHMC_SPEC_P 2
+#endif
+#ifndef RHMC_SPEC_Q
+#define RHMC_SPEC_Q 2
+#endif
+constexpr int kSpecP = RHMC_SPEC_P;
+constexpr int kSpecQ = RHMC_SPEC_Q;
+
 // 1/d to within ~11 ulp (v_rcp_f64 is accurate to ~2^-24; one Newton step).
 __device__ __forceinline__ double rcp_nr1(double d) {
   const double r = __builtin_amdgcn_rcp(d);
@@ -96,21 +106,42 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
     px = px - hdt * gx;
     py = py - hdt * gy;
     {                                              // :528-535 (dtaudq is 0 on x, y)
+      // SPEC_P iterations per pass; the state and count kept are those of the
+      // first iteration whose test stops the reference's loop.
       const double rho = pf, hc = hdt * (fm.coef * 0.5);
-      double dp;
       int n = 0;
+      bool more;
       do {
-        const double pp = fma(-hc, pf * pf, rho);
-        dp = fabs(pf - pp);
-        pf = pp;
-        ++n;
-      } while (dp > c.delta && n < c.counter_max);
+        double P[kSpecP + 1];
+        bool go[kSpecP];
+        P[0] = pf;
+#pragma unroll
+        for (int k = 0; k < kSpecP; ++k) {
+          P[k + 1] = fma(-hc, P[k] * P[k], rho);
+          go[k] = fabs(P[k] - P[k + 1]) > c.delta;
+        }
+        int take = kSpecP;
+        double sel = P[kSpecP];
+        more = go[kSpecP - 1];
+#pragma unroll
+        for (int k = kSpecP - 1; k >= 0; --k) {
+          if (!go[k] || n + k + 1 >= c.counter_max) {
+            take = k + 1;
+            sel = P[k + 1];
+            more = go[k];
+          }
+        }
+        pf = sel;
+        n += take;
+      } while (more && n < c.counter_max);
       it_p += n;
-      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
+      if (more) st |= RHMC_STATUS_PLOOP_CAP;
     }
     {                                              // :538-545
       // q_{n+1} = q_s + hdt (p/H(q_s) + p/H(q_n)) with 1/H_ff(f) = f/g_ff2 + c0
       // and 1/H_xx(f) = g(f)/g_xx, g = u/g1 + (B/g2) u^2: affine in f and g.
+      // The flux iterates are an affine recurrence, so SPEC_Q iterations per
+      // pass cost one dependent chain (their reciprocals overlap) and one branch.
       const double ihxx_s = fm.s * lc.inv_gxx;
       const double bf = hdt * (pf * lc.inv_gff2), cf = f + hdt * (pf * fm.A + pf * lc.c0);
       const double bx = hdt * (px * lc.inv_gxx), cx = x + hdt * (px * ihxx_s);
@@ -118,18 +149,43 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       bool more;
       int n = 0;
       do {
-        const double fl = (f < lc.f_low) ? lc.f_low : f;
-        const double u = rcp_nr1(fl);
-        const double g = u * fma(lc.Bg2, u, lc.inv_g1);
-        const double nf = fma(bf, f, cf), nx = fma(bx, g, cx), ny = fma(by, g, cy);
-        const double a0 = fabs(f - nf), a1 = fabs(x - nx), a2 = fabs(y - ny);
-        const double sum = a0 + a1 + a2;
-        // dq = np.max(...) > delta, NaN stops the loop
-        more = (fmax(fmax(a0, a1), a2) > c.delta) && (sum == sum);
-        f = nf;
-        x = nx;
-        y = ny;
-        ++n;
+        double F[kSpecQ + 1], X[kSpecQ + 1], Y[kSpecQ + 1];
+        bool go[kSpecQ];
+        F[0] = f;
+        X[0] = x;
+        Y[0] = y;
+#pragma unroll
+        for (int k = 0; k < kSpecQ; ++k) F[k + 1] = fma(bf, F[k], cf);
+#pragma unroll
+        for (int k = 0; k < kSpecQ; ++k) {
+          const double fl = (F[k] < lc.f_low) ? lc.f_low : F[k];
+          const double u = rcp_nr1(fl);
+          const double g = u * fma(lc.Bg2, u, lc.inv_g1);
+          X[k + 1] = fma(bx, g, cx);
+          Y[k + 1] = fma(by, g, cy);
+          const double a0 = fabs(F[k] - F[k + 1]), a1 = fabs(X[k] - X[k + 1]),
+                       a2 = fabs(Y[k] - Y[k + 1]);
+          const double sum = a0 + a1 + a2;
+          // dq = np.max(...) > delta, NaN stops the loop
+          go[k] = (fmax(fmax(a0, a1), a2) > c.delta) && (sum == sum);
+        }
+        int take = kSpecQ;
+        double sf = F[kSpecQ], sx = X[kSpecQ], sy = Y[kSpecQ];
+        more = go[kSpecQ - 1];
+#pragma unroll
+        for (int k = kSpecQ - 1; k >= 0; --k) {
+          if (!go[k] || n + k + 1 >= c.counter_max) {
+            take = k + 1;
+            sf = F[k + 1];
+            sx = X[k + 1];
+            sy = Y[k + 1];
+            more = go[k];
+          }
+        }
+        f = sf;
+        x = sx;
+        y = sy;
+        n += take;
       } while (more && n < c.counter_max);
       it_q += n;
       if (more) st |= RHMC_STATUS_QLOOP_CAP;

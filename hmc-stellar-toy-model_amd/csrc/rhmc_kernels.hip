@@ -32,6 +32,7 @@
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
 #include "rhmc_tiledk.hpp"
+#include "rhmc_tiledr.hpp"
 #include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -703,6 +704,9 @@ struct rhmc_ctx {
   hipStream_t stream = nullptr;
   int rows = 0, cols = 0;
   double* d_D = nullptr;
+  float* d_Df = nullptr;   // D in fp32, valid when img_f32
+  int* d_flag = nullptr;
+  bool img_f32 = false;    // every pixel of D is exactly representable in fp32
   // scratch for the host-pointer entry points
   void* scratch = nullptr;
   size_t scratch_bytes = 0;
@@ -744,12 +748,13 @@ int window_unsupported() {
               "that needs the windowed kernels (K > 16 or image larger than LDS)");
 }
 
-// RHMC_KERNEL=tiledw / tiledw32 force the windowed single-star kernel (16 / 32
-// lanes per chain), "tiled2"/"tiled1"
-// and the generic-LPC names below force full-image kernels.
+// Single-star kernel selection (RHMC_KERNEL): tiledr* = register-window
+// kernel (the default), tiledw / tiledw32 = LDS-operand window kernel with 16 /
+// 32 lanes per chain, tiled1 / tiled2 = full-image kernels.
 bool force_full_image_k1() {
   const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiled", 5) == 0;
+  return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiledr", 6) != 0 &&
+         std::strncmp(e, "tiled", 5) == 0;
 }
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
@@ -947,8 +952,42 @@ int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   return RHMC_OK;
 }
 
-// Lanes per chain of the windowed single-star kernel: 16 (4 chains per wave,
-// the default) or 32 (RHMC_KERNEL=tiledw32).
+// Register-window single-star kernel (rhmc_tiledr.hpp).
+template <int IMG, int WIN, typename DT, bool PROF>
+int launch_tiledr_t(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  using TL = TiledR<IMG, WIN, DT>;
+  const size_t lds = TL::lds_bytes();
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+  constexpr int W = 4;
+  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_k1_tiledr<IMG, WIN, DT, PROF>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+// Register-window kernel (rhmc_tiledr.hpp): the 28-pixel window when the PSF
+// allows it (RHMC_KERNEL=tiledr32 forces 32), the fp32 pixel cache when the
+// image allows it exactly (RHMC_KERNEL=tiledr64 forces fp64).
+template <int IMG>
+int launch_tiledr(const rhmc_ctx* ctx, LeapArgsK1 a, hipStream_t s) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  const bool w28 = reg_window_ok(28, a.c.inv_two_sig2) && !(e && std::strcmp(e, "tiledr32") == 0);
+  const bool f32 = ctx->img_f32 && !(e && std::strcmp(e, "tiledr64") == 0);
+  if (e && std::strcmp(e, "profr") == 0 && w28 && f32) {
+    a.Df = ctx->d_Df;
+    return launch_tiledr_t<IMG, 28, float, true>(ctx, a, s);
+  }
+  if (f32) {
+    a.Df = ctx->d_Df;
+    return w28 ? launch_tiledr_t<IMG, 28, float, false>(ctx, a, s)
+               : launch_tiledr_t<IMG, 32, float, false>(ctx, a, s);
+  }
+  return w28 ? launch_tiledr_t<IMG, 28, double, false>(ctx, a, s)
+             : launch_tiledr_t<IMG, 32, double, false>(ctx, a, s);
+}
+
+// Windowed single-star kernels: register-window (default, RHMC_KERNEL=tiledr)
+// or the LDS-operand kernel with 16 / 32 lanes per chain (tiledw / tiledw32).
 template <int IMG>
 int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   const char* e = std::getenv("RHMC_KERNEL");
@@ -1025,9 +1064,15 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   const int side = ctx->rows;
   const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
                   !force_windowed();
-  const bool k1w = k1 && window_exact(a.c) && !force_full_image_k1() &&
+  const char* ke = std::getenv("RHMC_KERNEL");
+  const bool img_ok = side == 32 || side == 48 || side == 64 || side == 96 || side == 128;
+  // register-window kernel (default) / LDS-operand window kernel (tiledw*)
+  const bool k1r = k1 && img_ok && !force_full_image_k1() && reg_window_ok(32, a.c.inv_two_sig2) &&
+                   !(ke && std::strncmp(ke, "tiledw", 6) == 0) &&
+                   !(ke && std::strncmp(ke, "profw", 5) == 0);
+  const bool k1w = !k1r && k1 && window_exact(a.c) && !force_full_image_k1() &&
                    (side == 48 || side == 64 || side == 96 || side == 128);
-  if (k1w || (k1 && (side == 16 || side == 32 || side == 48 || side == 64))) {
+  if (k1r || k1w || (k1 && (side == 16 || side == 32 || side == 48 || side == 64))) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -1039,7 +1084,17 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.rows = ctx->rows;
     t.cols = ctx->cols;
     t.pad = 0;
+    t.Df = nullptr;
     t.c = a.c;
+    if (k1r) {
+      switch (side) {
+        case 32: return launch_tiledr<32>(ctx, t, s);
+        case 48: return launch_tiledr<48>(ctx, t, s);
+        case 64: return launch_tiledr<64>(ctx, t, s);
+        case 96: return launch_tiledr<96>(ctx, t, s);
+        default: return launch_tiledr<128>(ctx, t, s);
+      }
+    }
     if (k1w) {
       switch (side) {
         case 48: return launch_tiledw<48>(ctx, t, s);
@@ -1221,6 +1276,46 @@ int launch_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int
 
 }  // namespace
 
+namespace {
+
+// fp32 copy of the image and whether it is exact (every pixel == (float)pixel,
+// NaN counts as inexact): the register-window kernel caches window pixels in
+// fp32 when it is (rhmc_tiledr.hpp).
+__global__ void image_f32_kernel(const double* __restrict__ D, float* __restrict__ Df,
+                                 int64_t n, int* __restrict__ inexact) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = D[i];
+    const float f = (float)v;
+    Df[i] = f;
+    if (!((double)f == v)) atomicOr(inexact, 1);
+  }
+}
+
+// Called with the new image already enqueued on ctx->stream; synchronises.
+int refresh_image_f32(rhmc_ctx* ctx) {
+  const int64_t n = (int64_t)ctx->rows * ctx->cols;
+  if (ctx->d_Df) HIP_TRY(hipFree(ctx->d_Df));
+  ctx->d_Df = nullptr;
+  ctx->img_f32 = false;
+  if (hipMalloc(&ctx->d_Df, (size_t)n * sizeof(float)) != hipSuccess)
+    return fail(RHMC_ERR_NOMEM, "hipMalloc fp32 image failed");
+  if (!ctx->d_flag && hipMalloc(&ctx->d_flag, sizeof(int)) != hipSuccess)
+    return fail(RHMC_ERR_NOMEM, "hipMalloc flag failed");
+  HIP_TRY(hipMemsetAsync(ctx->d_flag, 0, sizeof(int), ctx->stream));
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 1024);
+  hipLaunchKernelGGL(image_f32_kernel, dim3(blocks), dim3(256), 0, ctx->stream, ctx->d_D,
+                     ctx->d_Df, n, ctx->d_flag);
+  HIP_TRY(hipGetLastError());
+  int inexact = 1;
+  HIP_TRY(hipMemcpyAsync(&inexact, ctx->d_flag, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  ctx->img_f32 = inexact == 0;
+  return RHMC_OK;
+}
+
+}  // namespace
+
 extern "C" {
 
 int rhmc_abi_version(void) { return RHMC_ABI_VERSION; }
@@ -1251,9 +1346,11 @@ int rhmc_ctx_set_image(rhmc_ctx* ctx, const double* D, int32_t rows, int32_t col
   if (!ctx->d_D && hipMalloc(&ctx->d_D, bytes) != hipSuccess)
     return fail(RHMC_ERR_NOMEM, "hipMalloc image failed");
   HIP_TRY(hipMemcpyAsync(ctx->d_D, D, bytes, hipMemcpyHostToDevice, ctx->stream));
-  HIP_TRY(hipStreamSynchronize(ctx->stream));
   ctx->rows = rows;
   ctx->cols = cols;
+  int rc = refresh_image_f32(ctx);
+  if (rc) return rc;
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
   return RHMC_OK;
 }
 
@@ -1298,6 +1395,8 @@ void rhmc_ctx_destroy(rhmc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->d_D) (void)hipFree(ctx->d_D);
+  if (ctx->d_Df) (void)hipFree(ctx->d_Df);
+  if (ctx->d_flag) (void)hipFree(ctx->d_flag);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->mh_scratch) (void)hipFree(ctx->mh_scratch);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -1566,6 +1665,7 @@ int rhmc_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* q, int32_t
     HIP_TRY(hipMemcpyAsync(ctx->d_D, dout, bytes, hipMemcpyDeviceToDevice, ctx->stream));
     ctx->rows = rows;
     ctx->cols = cols;
+    if ((rc = refresh_image_f32(ctx))) return rc;
   }
   if (out) HIP_TRY(hipMemcpyAsync(out, dout, ob, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipStreamSynchronize(ctx->stream));

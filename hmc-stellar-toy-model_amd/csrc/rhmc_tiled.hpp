@@ -174,6 +174,7 @@ struct LeapArgsK1 {
   int32_t* fp_iters;
   int32_t* status;
   const double* D;
+  const float* Df;   // D in fp32 when exact (ctx->img_f32), else nullptr
   int64_t n_chains;
   int n_steps, rows, cols, pad;
   Consts c;

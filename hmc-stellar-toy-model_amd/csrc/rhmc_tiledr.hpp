@@ -1,0 +1,272 @@
+// rhmc_tiledr.hpp — single-star leapfrog on a WIN x WIN pixel window per
+// chain (WIN = 28 or 32) with the window's data pixels held in REGISTERS
+// across steps: 16 lanes per chain, 4 chains per wave64.
+//
+// Window.  Rows o_x .. o_x + WIN - 1 with o_x = floor(x + 0.5) - WIN/2 (then
+// clamped into the image), likewise columns: every pixel centre left out is
+// >= WIN/2 px from the star, where PSF/peak = exp(-(WIN/2)^2 / (2 sigma^2)).
+// launch_leapfrog uses a window only when that is <= 2^-62 (WIN = 28:
+// sigma <= 1.510 px; WIN = 32: sigma <= 1.726 px; the reference PSF has
+// sigma = 3.5/2.354 = 1.487 px, 2^-64 at WIN = 28).  A dropped pixel then
+// changes neither its Lambda (f PSF < half an ulp of B for f < 4e5 counts)
+// nor the gradient sums beyond their own rounding (every dropped term is
+// < 2^-62 of the peak pixel's term; together they stay below one ulp of it).
+//
+// Operands live in registers, not LDS:
+//  * D: the window moves only when round(x) or round(y) changes, so each lane
+//    keeps its TR x TC window pixels in VGPRs and re-reads them from the LDS
+//    copy of the image only on such a step (a wave-uniform branch: a divergent
+//    one would keep the old values live through the loads and double the
+//    register footprint).  The cache is fp32 when every image pixel is exactly
+//    representable (Poisson counts < 2^24, checked when the image is set: one
+//    exact v_cvt_f64_f32 per use), else fp64.
+//  * PSF factors: lane (a, b) (a = m / 4, b = m % 4) owns window rows
+//    a TR .. a TR + TR - 1 and window columns b, b + 4, ..., b + 4 (TC - 1).
+//    Quad-mates (same a) share rows: lane b evaluates rows a TR + b + {0, 4}
+//    and DPP quad broadcasts hand them round.  Lanes with the same b share
+//    columns: lane a evaluates columns b + 4 (a + {0, 4}) and ds_swizzle in
+//    bit mode (and 0x13, or a' << 2: "lane (a', b) of my 16-lane group")
+//    hands them round.  Four exps per lane, static slot maps, no LDS tables.
+//  * Position moments with offsets linear in the index:
+//    sum_i w_i ((o + a TR + i) - x + 0.5) = dxa sum_i w_i + sum_i i w_i.
+//
+// Reference: dphidq / dVdq sampler_RHMC.py:365-425, :448-465; the step loop is
+// rhmc_k1step.hpp (:522-566).
+#pragma once
+#include "rhmc_exp.hpp"
+#include "rhmc_k1step.hpp"
+#include "rhmc_tiled.hpp"
+#include "rhmc_tiled2.hpp"
+#include "rhmc_wave.hpp"
+#include "rhmc_windowed.hpp"
+
+namespace rhmc {
+
+// exp(-(WIN/2)^2 / (2 sigma^2)) <= 2^-62 (62 ln 2 = 42.975)?
+__host__ __device__ inline bool reg_window_ok(int win, double inv_two_sig2) {
+  const double h = 0.5 * win;
+  return h * h * inv_two_sig2 >= 42.98;
+}
+
+template <int PAT>
+__device__ __forceinline__ double swizzle_d(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)b, PAT);
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), PAT);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// DT: the type the window pixels are cached in (float when the image is
+// exactly representable in fp32, else double).
+template <int IMG, int WIN, typename DT>
+struct TiledR {
+  static constexpr int LPC = 16;           // lanes per chain
+  static constexpr int CPW = kWave / LPC;  // chains per wave
+  static constexpr int P = IMG + 1;        // LDS row pitch
+  static constexpr int TR = WIN / 4;       // window rows per lane
+  static constexpr int TC = WIN / 4;       // window columns per lane
+  static constexpr int NPX = TR * TC;
+  static_assert(WIN == 28 || WIN == 32, "window side");
+  static_assert(IMG >= WIN, "window inside the image");
+
+  // LDS: the exp table (64 doubles), then the image as DT [IMG][P].
+  static __host__ __device__ constexpr size_t lds_bytes() {
+    return kExpTab * sizeof(double) + (size_t)IMG * P * sizeof(DT);
+  }
+  static __device__ __forceinline__ int origin(double v) {
+    if (!(fabs(v) < 1.0e7)) return 0;
+    const int o = (int)floor(v + 0.5) - WIN / 2;
+    return o < 0 ? 0 : (o > IMG - WIN ? IMG - WIN : o);
+  }
+
+  // 16-lane all-reduce (DPP inside a row); every lane of the chain gets the sum.
+  static __device__ __forceinline__ double group_sum(double v) {
+    v += dpp_move<0xB1>(v);   // quad_perm [1,0,3,2]
+    v += dpp_move<0x4E>(v);   // quad_perm [2,3,0,1]
+    v += dpp_move<0x141>(v);  // row_half_mirror
+    v += dpp_move<0x140>(v);  // row_mirror
+    return v;
+  }
+
+  // Window pixels of this lane and the window origin they belong to.
+  struct Cache {
+    DT d[NPX];
+    int r0, c0;
+  };
+  static __device__ __forceinline__ void init(Cache& k) {
+    k.r0 = -1;
+    k.c0 = -1;
+  }
+
+  // value of quad lane J (rows) / of lane (J, b) of the 16-lane group (columns)
+  template <int J>
+  static __device__ __forceinline__ double row_bcast(double v) {
+    return dpp_move<J | (J << 2) | (J << 4) | (J << 6)>(v);
+  }
+  template <int J>
+  static __device__ __forceinline__ double col_bcast(double v) {
+    return swizzle_d<0x13 | ((J << 2) << 5)>(v);
+  }
+
+  // Pixel part of the chain's dphidq (every lane of the chain gets it).
+  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
+                                                  const DT* __restrict__ sD, Cache& k,
+                                                  double f, double x, double y, const Consts& c,
+                                                  const LeanConsts& lc, double& gf, double& gx,
+                                                  double& gy) {
+    const int m = lane_id() % LPC;
+    const int a = m / 4, b = m % 4;
+    const int r0 = origin(x), c0 = origin(y);
+    if (__builtin_amdgcn_ballot_w64(r0 != k.r0 || c0 != k.c0) != 0) {
+      const DT* base = sD + (r0 + TR * a) * P + c0 + b;
+#pragma unroll
+      for (int i = 0; i < TR; ++i)
+#pragma unroll
+        for (int j = 0; j < TC; ++j) k.d[i * TC + j] = base[i * P + 4 * j];
+      k.r0 = r0;
+      k.c0 = c0;
+    }
+    // PSF factors: 2 rows + 2 columns per lane, then broadcast.
+    double rv[2], cv[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int er = TR * a + b + 4 * t;
+      const double vr = ((r0 + er) + 0.5) - x;
+      rv[t] = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
+      const int ec = b + 4 * (a + 4 * t);
+      const double vc = ((c0 + ec) + 0.5) - y;
+      cv[t] = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
+    }
+    double ex[TR], ey[TC];
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+      const double v = rv[i / 4];
+      ex[i] = (i % 4 == 0) ? row_bcast<0>(v)
+            : (i % 4 == 1) ? row_bcast<1>(v)
+            : (i % 4 == 2) ? row_bcast<2>(v) : row_bcast<3>(v);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const double v = cv[j / 4];
+      ey[j] = (j % 4 == 0) ? col_bcast<0>(v)
+            : (j % 4 == 1) ? col_bcast<1>(v)
+            : (j % 4 == 2) ? col_bcast<2>(v) : col_bcast<3>(v);
+    }
+
+    // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per pixel pair (row-major
+    // pairs), and the separable row / column sums (rhmc_tiled2.hpp).
+    double R[TR], C[TC], fe[TR];
+#pragma unroll
+    for (int i = 0; i < TR; ++i) fe[i] = f * ex[i];
+#pragma unroll
+    for (int pp = 0; pp + 1 < NPX; pp += 2) {
+      const int i1 = pp / TC, j1 = pp % TC, i2 = (pp + 1) / TC, j2 = (pp + 1) % TC;
+      const double d1 = (double)k.d[pp], d2 = (double)k.d[pp + 1];
+      const double l1 = fma(fe[i1], ey[j1], c.B), l2 = fma(fe[i2], ey[j2], c.B);  // :373-376
+      const double L = l1 * l2;
+      double r = __builtin_amdgcn_rcp(L);
+      r = fma(r, fma(-L, r, 1.0), r);
+      const double s1 = fma(d1, l2 * r, -1.0), s2 = fma(d2, l1 * r, -1.0);  // :379
+      R[i1] = (j1 == 0) ? ey[j1] * s1 : fma(ey[j1], s1, R[i1]);
+      C[j1] = (i1 == 0) ? ex[i1] * s1 : fma(ex[i1], s1, C[j1]);
+      R[i2] = (j2 == 0) ? ey[j2] * s2 : fma(ey[j2], s2, R[i2]);
+      C[j2] = (i2 == 0) ? ex[i2] * s2 : fma(ex[i2], s2, C[j2]);
+    }
+    if constexpr (NPX % 2 == 1) {  // last pixel on its own
+      constexpr int pp = NPX - 1, i1 = pp / TC, j1 = pp % TC;
+      const double d1 = (double)k.d[pp];
+      const double l1 = fma(fe[i1], ey[j1], c.B);
+      double r = __builtin_amdgcn_rcp(l1);
+      r = fma(r, fma(-l1, r, 1.0), r);
+      const double s1 = fma(d1, r, -1.0);
+      R[i1] = fma(ey[j1], s1, R[i1]);
+      C[j1] = fma(ex[i1], s1, C[j1]);
+    }
+    double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+      const double tt = ex[i] * R[i];
+      a0 += tt;
+      a1 = fma(tt, (double)i, a1);
+    }
+#pragma unroll
+    for (int j = 0; j < TC; ++j) {
+      const double w = ey[j] * C[j];
+      w0 += w;
+      w1 = fma(w, (double)(4 * j), w1);
+    }
+    const double dxa = ((double)(r0 + TR * a) - x) + 0.5;  // offset of the lane's row 0
+    const double dyb = ((double)(c0 + b) - y) + 0.5;       // offset of the lane's column 0
+    const double s0 = group_sum(a0);
+    const double s1 = group_sum(fma(dxa, a0, a1));
+    const double s2 = group_sum(fma(dyb, w0, w1));
+    gf = -s0;                                          // :404
+    gx = -s1 * f * lc.inv_var;                         // :405
+    gy = -s2 * f * lc.inv_var;                         // :406
+  }
+};
+
+// One wave = 4 chains x 16 lanes; W waves per workgroup share the LDS image.
+template <int IMG, int WIN, typename DT, bool PROF = false>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+leapfrog_k1_tiledr(LeapArgsK1 a) {
+  using TL = TiledR<IMG, WIN, DT>;
+  extern __shared__ double lds[];
+  DT* simg = reinterpret_cast<DT*>(lds + kExpTab);
+  const DT* gimg;
+  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
+  else gimg = reinterpret_cast<const DT*>(a.D);
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) {
+    const int r = e / IMG, cc = e - (e / IMG) * IMG;
+    simg[r * TL::P + cc] = gimg[e];
+  }
+  exp_tab_fill(lds);
+  __syncthreads();
+  const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (TL::CPW * wave >= a.n_chains) return;
+  const int lane = lane_id();
+  const int h = lane / TL::LPC;
+  const int64_t chain = TL::CPW * wave + h;
+  const bool real = chain < a.n_chains;            // ragged tail: mirror the wave's first chain
+  const int64_t base = (real ? chain : TL::CPW * wave) * 3;
+
+  double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+  const LeanConsts lc = lean_consts(c);
+  typename TL::Cache cache;
+  TL::init(cache);
+  int it_p = 0, it_q = 0;
+  unsigned st = 0u;
+  long long prof[2] = {0, 0};
+  k1_steps<PROF>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
+                 [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
+                   TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
+                 },
+                 it_p, it_q, st, prof);
+  if constexpr (PROF) {
+    const int ns = a.n_steps > 0 ? a.n_steps : 1;
+    it_p = (int)(prof[0] / ns);
+    it_q = (int)(prof[1] / ns);
+  }
+
+  if ((lane % TL::LPC) == 0 && real) {
+    if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
+          isfinite(py)))
+      st |= RHMC_STATUS_NONFINITE;
+    a.q[base] = f;
+    a.q[base + 1] = x;
+    a.q[base + 2] = y;
+    a.p[base] = pf;
+    a.p[base + 1] = px;
+    a.p[base + 2] = py;
+    if (a.status) a.status[chain] = (int32_t)st;
+    if (a.fp_iters) {
+      a.fp_iters[2 * chain] = it_p;
+      a.fp_iters[2 * chain + 1] = it_q;
+    }
+  }
+}
+
+}  // namespace rhmc

@@ -35,6 +35,23 @@ __global__ void thr(double* out, double seed, int iters) {
     } else if (MODE == 5) {  // rcp mixed 1:6 with fma (pixel-loop ratio)
       a0 = __builtin_amdgcn_rcp(a0); a1 = fma(a1, m, c); a2 = fma(a2, m, c); a3 = fma(a3, m, c);
       a4 = fma(a4, m, c); a5 = fma(a5, m, c); a6 = fma(a6, m, c); a7 = fma(a7, m, c);
+    } else if (MODE == 7) {  // rcp dependent chain (latency)
+      a0 = __builtin_amdgcn_rcp(a0); a0 = __builtin_amdgcn_rcp(a0);
+      a0 = __builtin_amdgcn_rcp(a0); a0 = __builtin_amdgcn_rcp(a0);
+      a0 = __builtin_amdgcn_rcp(a0); a0 = __builtin_amdgcn_rcp(a0);
+      a0 = __builtin_amdgcn_rcp(a0); a0 = __builtin_amdgcn_rcp(a0);
+    } else if (MODE == 8) {  // 8 independent f32 -> f64 conversions
+      a0 = (double)(float)a1; a1 = (double)(float)a2; a2 = (double)(float)a3;
+      a3 = (double)(float)a4; a4 = (double)(float)a5; a5 = (double)(float)a6;
+      a6 = (double)(float)a7; a7 = (double)(float)a0;
+    } else if (MODE == 9) {  // dependent add chain through a DPP move (quad_perm)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const long long b = __double_as_longlong(a0);
+        const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
+        const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0xB1, 0xF, 0xF, false);
+        a0 = a0 * m + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+      }
     } else if (MODE == 6) {  // exp (ocml) x8 independent
       a0 = exp(-a0); a1 = exp(-a1); a2 = exp(-a2); a3 = exp(-a3);
       a4 = exp(-a4); a5 = exp(-a5); a6 = exp(-a6); a7 = exp(-a7);
@@ -109,11 +126,12 @@ int main() {
   const int simds = prop.multiProcessorCount * 4;
   const double ghz = 2.4;
   const char* names[] = {"fma x8 indep", "rcp x8 indep", "fma dep chain", "fma 2 chains",
-                         "mul x8 indep", "rcp:fma 1:7", "exp x8 indep"};
+                         "mul x8 indep", "rcp:fma 1:7", "exp x8 indep", "rcp dep chain",
+                         "cvt f32->f64 x8", "dpp+fma dep x8"};
   const int iters = 20000;
   for (int wps : {1, 2, 4}) {
     const int blocks = simds * wps;
-    float t[7];
+    float t[10];
     t[0] = run<0>(blocks, iters);
     t[1] = run<1>(blocks, iters);
     t[2] = run<2>(blocks, iters);
@@ -121,7 +139,10 @@ int main() {
     t[4] = run<4>(blocks, iters);
     t[5] = run<5>(blocks, iters);
     t[6] = run<6>(blocks, iters / 20);
-    for (int m = 0; m < 7; ++m) {
+    t[7] = run<7>(blocks, iters);
+    t[8] = run<8>(blocks, iters);
+    t[9] = run<9>(blocks, iters);
+    for (int m = 0; m < 10; ++m) {
       const double ops = (double)wps * iters / (m == 6 ? 20 : 1) * 8;  // wave-ops per SIMD
       printf("waves/SIMD %d  %-14s %8.3f ms  %6.2f cycles/wave-op @%.1fGHz\n", wps, names[m],
              t[m], t[m] * 1e-3 * ghz * 1e9 / ops, ghz);

@@ -21,7 +21,7 @@ for _ in range(2):
 torch.cuda.synchronize()
 a = it.cpu().numpy().astype(float)
 b = st.cpu().numpy().astype(float)
-if os.environ.get("RHMC_KERNEL", "").startswith("profw"):
+if os.environ.get("RHMC_KERNEL", "").startswith(("profw", "profr")):
     print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
         os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), a.sum(1).mean()))
 else:
