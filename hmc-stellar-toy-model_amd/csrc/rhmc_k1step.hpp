@@ -13,6 +13,11 @@
 #include "rhmc.h"
 #include "rhmc_wave.hpp"
 
+#ifdef RHMC_MARKS
+#define RHMC_MARK(n) asm volatile("s_setprio " #n ::: "memory")
+#else
+#define RHMC_MARK(n)
+#endif
 namespace rhmc {
 
 // Fixed-point iterations evaluated per pass (one branch per pass).
@@ -76,7 +81,9 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (s > 0) prof[1] += t1 - t0;
       t0 = t1;
     }
+    RHMC_MARK(1);
     grad(f, x, y, gf, gx, gy);
+    RHMC_MARK(2);
     if constexpr (PROF) {
       const long long t1 = clock64();
       prof[0] += t1 - t0;
@@ -136,6 +143,7 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       } while (more && n < c.counter_max);
       it_p += n;
       if (more) st |= RHMC_STATUS_PLOOP_CAP;
+      RHMC_MARK(3);
     }
     {                                              // :538-545
       // q_{n+1} = q_s + hdt (p/H(q_s) + p/H(q_n)) with 1/H_ff(f) = f/g_ff2 + c0
@@ -189,9 +197,11 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       } while (more && n < c.counter_max);
       it_q += n;
       if (more) st |= RHMC_STATUS_QLOOP_CAP;
+      RHMC_MARK(4);
     }
     fm = flux_metric(f, c, lc);
     pf = pf - hdt * ((pf * pf) * fm.coef / 2.0);   // :548
+    RHMC_MARK(5);
   }
 }
 

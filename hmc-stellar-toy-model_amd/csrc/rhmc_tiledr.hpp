@@ -88,14 +88,29 @@ struct TiledR {
     return v;
   }
 
-  // Window pixels of this lane and the window origin they belong to.
+  // Window pixels of this lane, the window origin they belong to (as doubles)
+  // and the coordinate ranges over which that origin stays the same:
+  // x in [xlo, xhi) implies floor(x + 0.5) == the cached unclamped origin
+  // (xhi sits 2^-40 below the rounding boundary so that the rounded x + 0.5
+  // cannot reach it; a false "moved" only costs a reload).
   struct Cache {
     DT d[NPX];
-    int r0, c0;
+    double r0, c0;
+    double xlo, xhi, ylo, yhi;
   };
   static __device__ __forceinline__ void init(Cache& k) {
-    k.r0 = -1;
-    k.c0 = -1;
+    k.xlo = k.ylo = INFINITY;  // first step loads
+    k.xhi = k.yhi = -INFINITY;
+  }
+  static __device__ __forceinline__ void bounds(double v, double& lo, double& hi) {
+    if (!(fabs(v) < 1.0e7)) {  // absurd / NaN coordinate: re-check every step
+      lo = INFINITY;
+      hi = -INFINITY;
+      return;
+    }
+    const double o = floor(v + 0.5);
+    lo = o - 0.5;
+    hi = (o + 0.5) - 0x1p-40;
   }
 
   // value of quad lane J (rows) / of lane (J, b) of the 16-lane group (columns)
@@ -116,25 +131,29 @@ struct TiledR {
                                                   double& gy) {
     const int m = lane_id() % LPC;
     const int a = m / 4, b = m % 4;
-    const int r0 = origin(x), c0 = origin(y);
-    if (__builtin_amdgcn_ballot_w64(r0 != k.r0 || c0 != k.c0) != 0) {
+    const bool stay = x >= k.xlo && x < k.xhi && y >= k.ylo && y < k.yhi;
+    if (__builtin_amdgcn_ballot_w64(!stay) != 0) {
+      const int r0 = origin(x), c0 = origin(y);
       const DT* base = sD + (r0 + TR * a) * P + c0 + b;
 #pragma unroll
       for (int i = 0; i < TR; ++i)
 #pragma unroll
         for (int j = 0; j < TC; ++j) k.d[i * TC + j] = base[i * P + 4 * j];
-      k.r0 = r0;
-      k.c0 = c0;
+      k.r0 = (double)r0;
+      k.c0 = (double)c0;
+      bounds(x, k.xlo, k.xhi);
+      bounds(y, k.ylo, k.yhi);
     }
+    const double r0 = k.r0, c0 = k.c0;
     // PSF factors: 2 rows + 2 columns per lane, then broadcast.
     double rv[2], cv[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const int er = TR * a + b + 4 * t;
-      const double vr = ((r0 + er) + 0.5) - x;
+      const double er = (double)(TR * a + b + 4 * t) + 0.5;  // exact: (r0 + e) + 0.5
+      const double vr = (r0 + er) - x;
       rv[t] = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
-      const int ec = b + 4 * (a + 4 * t);
-      const double vc = ((c0 + ec) + 0.5) - y;
+      const double ec = (double)(b + 4 * (a + 4 * t)) + 0.5;
+      const double vc = (c0 + ec) - y;
       cv[t] = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
     }
     double ex[TR], ey[TC];
@@ -195,8 +214,8 @@ struct TiledR {
       w0 += w;
       w1 = fma(w, (double)(4 * j), w1);
     }
-    const double dxa = ((double)(r0 + TR * a) - x) + 0.5;  // offset of the lane's row 0
-    const double dyb = ((double)(c0 + b) - y) + 0.5;       // offset of the lane's column 0
+    const double dxa = ((r0 + (double)(TR * a)) - x) + 0.5;  // offset of the lane's row 0
+    const double dyb = ((c0 + (double)b) - y) + 0.5;         // offset of the lane's column 0
     const double s0 = group_sum(a0);
     const double s1 = group_sum(fma(dxa, a0, a1));
     const double s2 = group_sum(fma(dyb, w0, w1));
