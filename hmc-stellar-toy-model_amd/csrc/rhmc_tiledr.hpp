@@ -56,6 +56,12 @@ __device__ __forceinline__ double swizzle_d(double v) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// Pixels sharing one v_rcp_f64 in the pixel loop (2 or 4).
+#ifndef RHMC_RCP_GROUP
+#define RHMC_RCP_GROUP 2
+#endif
+constexpr int kRcpGroup = RHMC_RCP_GROUP;
+
 // DT: the type the window pixels are cached in (float when the image is
 // exactly representable in fp32, else double).
 template <int IMG, int WIN, typename DT>
@@ -172,34 +178,55 @@ struct TiledR {
             : (j % 4 == 2) ? col_bcast<2>(v) : col_bcast<3>(v);
     }
 
-    // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per pixel pair (row-major
-    // pairs), and the separable row / column sums (rhmc_tiled2.hpp).
+    // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
+    // pixels (row-major): 1/(l0 l1 l2 l3) by v_rcp_f64 + one Newton step, then
+    // 1/l0 = l1 l2 l3 r etc. by products (v_rcp_f64 issues at a quarter of the
+    // FMA rate); then the separable row / column sums (rhmc_tiled2.hpp).
     double R[TR], C[TC], fe[TR];
 #pragma unroll
     for (int i = 0; i < TR; ++i) fe[i] = f * ex[i];
+    auto lam = [&](int pp) {  // Lambda at pixel pp (:373-376)
+      return fma(fe[pp / TC], ey[pp % TC], c.B);
+    };
+    auto acc = [&](int pp, double sv) {  // row / column sums of s (D/Lambda - 1, :379)
+      const int i = pp / TC, j = pp % TC;
+      R[i] = (j == 0) ? ey[j] * sv : fma(ey[j], sv, R[i]);
+      C[j] = (i == 0) ? ex[i] * sv : fma(ex[i], sv, C[j]);
+    };
+    auto rcpn = [](double L) {
+      const double r = __builtin_amdgcn_rcp(L);
+      return fma(r, fma(-L, r, 1.0), r);
+    };
+    constexpr int G = kRcpGroup;
+    constexpr int NG = NPX / G * G;
 #pragma unroll
-    for (int pp = 0; pp + 1 < NPX; pp += 2) {
-      const int i1 = pp / TC, j1 = pp % TC, i2 = (pp + 1) / TC, j2 = (pp + 1) % TC;
-      const double d1 = (double)k.d[pp], d2 = (double)k.d[pp + 1];
-      const double l1 = fma(fe[i1], ey[j1], c.B), l2 = fma(fe[i2], ey[j2], c.B);  // :373-376
-      const double L = l1 * l2;
-      double r = __builtin_amdgcn_rcp(L);
-      r = fma(r, fma(-L, r, 1.0), r);
-      const double s1 = fma(d1, l2 * r, -1.0), s2 = fma(d2, l1 * r, -1.0);  // :379
-      R[i1] = (j1 == 0) ? ey[j1] * s1 : fma(ey[j1], s1, R[i1]);
-      C[j1] = (i1 == 0) ? ex[i1] * s1 : fma(ex[i1], s1, C[j1]);
-      R[i2] = (j2 == 0) ? ey[j2] * s2 : fma(ey[j2], s2, R[i2]);
-      C[j2] = (i2 == 0) ? ex[i2] * s2 : fma(ex[i2], s2, C[j2]);
+    for (int pp = 0; pp < NG; pp += G) {
+      if constexpr (G == 4) {
+        const double l0 = lam(pp), l1 = lam(pp + 1), l2 = lam(pp + 2), l3 = lam(pp + 3);
+        const double l01 = l0 * l1, l23 = l2 * l3;
+        const double r = rcpn(l01 * l23);
+        const double r01 = l23 * r, r23 = l01 * r;
+        acc(pp, fma((double)k.d[pp], l1 * r01, -1.0));
+        acc(pp + 1, fma((double)k.d[pp + 1], l0 * r01, -1.0));
+        acc(pp + 2, fma((double)k.d[pp + 2], l3 * r23, -1.0));
+        acc(pp + 3, fma((double)k.d[pp + 3], l2 * r23, -1.0));
+      } else {
+        const double l0 = lam(pp), l1 = lam(pp + 1);
+        const double r = rcpn(l0 * l1);
+        acc(pp, fma((double)k.d[pp], l1 * r, -1.0));
+        acc(pp + 1, fma((double)k.d[pp + 1], l0 * r, -1.0));
+      }
     }
-    if constexpr (NPX % 2 == 1) {  // last pixel on its own
-      constexpr int pp = NPX - 1, i1 = pp / TC, j1 = pp % TC;
-      const double d1 = (double)k.d[pp];
-      const double l1 = fma(fe[i1], ey[j1], c.B);
-      double r = __builtin_amdgcn_rcp(l1);
-      r = fma(r, fma(-l1, r, 1.0), r);
-      const double s1 = fma(d1, r, -1.0);
-      R[i1] = fma(ey[j1], s1, R[i1]);
-      C[j1] = fma(ex[i1], s1, C[j1]);
+    if constexpr (NPX - NG >= 2) {
+      constexpr int pp = NG;
+      const double l0 = lam(pp), l1 = lam(pp + 1);
+      const double r = rcpn(l0 * l1);
+      acc(pp, fma((double)k.d[pp], l1 * r, -1.0));
+      acc(pp + 1, fma((double)k.d[pp + 1], l0 * r, -1.0));
+    }
+    if constexpr ((NPX - NG) % 2 == 1) {  // last pixel on its own
+      constexpr int pp = NPX - 1;
+      acc(pp, fma((double)k.d[pp], rcpn(lam(pp)), -1.0));
     }
     double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll
