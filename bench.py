@@ -162,8 +162,8 @@ def bench_datagen(args, wl, P, ctx, dev, stream, world, rank):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C2")
     ap.add_argument("--chains", type=int, default=None, help="chains per GPU (weak scaling)")
     ap.add_argument("--global-chains", type=int, default=None,
@@ -319,6 +319,8 @@ def main():
         "achieved": fpc * chain_steps / (launch_ms * 1e-3) / 1e12,
         "frac": fpc * chain_steps / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
         "executed_fp64_flops_per_chain_step": fpc,
+        "valu_active_frac": pmc.get("valu_active_frac"),
+        "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
     }
     if rank == 0:
         out["cpu_baseline"] = cpu

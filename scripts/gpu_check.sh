@@ -21,6 +21,6 @@ if [ "$MODE" = all ] || [ "$MODE" = test ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step 600 bench python3 bench.py
-  step 600 rocprof rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+  step 600 rocprof rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu
 fi
 echo done

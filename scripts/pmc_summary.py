@@ -39,6 +39,10 @@ if all(k in avg for k in f64):
     out["fp64_flops_per_chain_step"] = flops / chain_steps
     out["valu_insts_per_chain_step"] = avg.get("SQ_INSTS_VALU", 0) / chain_steps
     out["fp64_insts_per_chain_step"] = sum(avg[k] for k in f64) / chain_steps
+if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg:
+    # fraction of the waves' lifetime with a VALU instruction issuing (both in
+    # quad-cycles); with one wave per SIMD this is the SIMD's VALU busy share
+    out["valu_active_frac"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
 if "GRBM_GUI_ACTIVE" in avg:
     out["note_clock"] = "effective clock = GRBM_GUI_ACTIVE / 8 / kernel time"
 dst = os.path.join("profiles", "pmc_%s.json" % wl)
