@@ -205,12 +205,15 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # RHMC_BENCH_DEVICE pins every rank to one device (rehearsing the N-rank
+    # path on a one-GPU box); by default rank r of a node uses GPU r.
+    gpu = int(os.environ.get("RHMC_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
 
     leap = args.leap or wl.n_steps
     P = capi.make_params(**wl.params)
-    ctx = capi.Context(wl.D, device=local_rank)
+    ctx = capi.Context(wl.D, device=gpu)
     q = torch.from_numpy(wl.q0).to(dev).contiguous()
     p = torch.from_numpy(wl.p0).to(dev).contiguous()
     it = torch.zeros((wl.n_chains, 2), dtype=torch.int32, device=dev)
