@@ -473,8 +473,10 @@ __global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
   // Infinite potential outside the support (:303-317)
   bool bad = false;
   if (owner) {
-    if (a.f_pos && f < c.f_lim) bad = true;
-    if (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)) bad = true;
+    if ((a.f_pos & RHMC_V_FLUX_WALL) && f < c.f_lim) bad = true;
+    if (!(a.f_pos & RHMC_V_NO_POSCHECK) &&
+        (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)))
+      bad = true;
   }
   if (__any(bad)) {
     if (lane == 0) a.V[chain] = INFINITY;
@@ -601,6 +603,65 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
   store_chain(a, chain, base, owner, s, 0, 0, st);
 }
 
+// samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552):
+// unit-mass leapfrog with a per-coordinate step vector dt[3K] and a per-chain
+// trajectory length steps[chain] >= 1, flux wall at c.f_lim with the
+// reference's quirks kept: the flip mask `iflip` is never cleared within a
+// trajectory (a star once below the wall has its flux momentum flipped on
+// every later step in which ANY star is below it, :529-541), and when the
+// last step flipped, p_tmp keeps the momentum the trajectory started from
+// (:547-550 update p_half, not p_tmp) — status bit RHMC_STATUS_REFLECT_F
+// marks those chains.  One wave per chain, lane k < K owns star k.
+__global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
+                                                             const double* __restrict__ dtv,
+                                                             const int32_t* __restrict__ steps) {
+  extern __shared__ double lds[];
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (chain >= a.n_chains) return;
+  const int K = a.K;
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const LeanConsts lc = lean_consts(c);
+  const int lane = lane_id();
+  const bool owner = lane < K;
+  int64_t base;
+  StarState s = load_chain(a, chain, K, owner, base);
+  const int rows = a.g.rows, cols = a.g.cols;
+  const int ks = owner ? lane : 0;
+  const double dtf = dtv[3 * ks], dtx = dtv[3 * ks + 1], dty = dtv[3 * ks + 2];
+  double gf, gx, gy;
+  win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+  double hf = s.pf - dtf * gf / 2.0, hx = s.px - dtx * gx / 2.0,  // :519
+         hy = s.py - dty * gy / 2.0;
+  bool iflip = false, flip = false;
+  const int n = steps[chain];
+  for (int t = 0; t < n; ++t) {
+    s.f = s.f + dtf * hf;                                             // :523
+    s.x = s.x + dtx * hx;
+    s.y = s.y + dty * hy;
+    const bool below = owner && s.f < c.f_lim;                        // :526-529
+    iflip = iflip || below;
+    flip = __builtin_amdgcn_ballot_w64(below) != 0;
+    win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+    const double kept = -hf;                                          // :531
+    hf = hf - dtf * gf;                                               // :532, :535
+    hx = hx - dtx * gx;
+    hy = hy - dty * gy;
+    if (flip && iflip) hf = kept;                                     // :533
+  }
+  unsigned st = 0u;
+  if (flip) {
+    st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
+  } else {                        // :551-552, dVdq at the same q as the last step
+    s.pf = hf + dtf * gf / 2.0;
+    s.px = hx + dtx * gx / 2.0;
+    s.py = hy + dty * gy / 2.0;
+  }
+  store_chain(a, chain, base, owner, s, 0, 0, st);
+}
+
 // Large-image gradient (windowed), one wave per chain.
 __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   extern __shared__ double lds[];
@@ -656,8 +717,10 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   if (!a.V) return;
   bool bad = false;
   if (owner) {
-    if (a.f_pos && f < c.f_lim) bad = true;
-    if (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)) bad = true;
+    if ((a.f_pos & RHMC_V_FLUX_WALL) && f < c.f_lim) bad = true;
+    if (!(a.f_pos & RHMC_V_NO_POSCHECK) &&
+        (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)))
+      bad = true;
   }
   if (__any(bad)) {
     if (lane == 0) a.V[chain] = INFINITY;
@@ -1018,7 +1081,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.D = ctx->d_D;
   a.n_chains = n;
   a.K = K;
-  a.f_pos = f_pos != 0;
+  a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
@@ -1188,6 +1251,7 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   m.K = K;
   m.seed = seed;
   m.c = c;
+  f_pos = f_pos != 0 ? RHMC_V_FLUX_WALL : 0;
   if ((rc = launch_energy(ctx, c, d_q, nullptr, m.V_cur, nullptr, n, K, f_pos, s))) return rc;
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
   for (int it = 0; it < n_iter; ++it) {
@@ -1239,6 +1303,34 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   else
     hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_RHMC_LEAPFROG>, grid, block, lds, s, a,
                        fp);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
+int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, double* d_q,
+                      double* d_p, const int32_t* d_steps, int64_t n, int32_t K, int32_t* d_st,
+                      hipStream_t s) {
+  LeapArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  if (n == 0) return RHMC_OK;
+  if (!d_dt || !d_steps) return fail(RHMC_ERR_ARG, "dt/steps is NULL");
+  if (!window_exact(a.c)) return window_unsupported();  // windowed gradient
+  a.q = d_q;
+  a.p = d_p;
+  a.fp_iters = nullptr;
+  a.status = d_st;
+  a.D = ctx->d_D;
+  a.n_chains = n;
+  a.K = K;
+  a.n_steps = 0;
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  size_t lds;
+  int W;
+  pick_waves_win(ctx, K, &lds, &W);
+  HIP_TRY(hipSetDevice(ctx->device));
+  const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL(hmc_random_win_kernel, grid, block, lds, s, a, d_dt, d_steps);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -1611,6 +1703,49 @@ int rhmc_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* 
   HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
   if ((rc = launch_integrate(ctx, P, solver, dq, dp, n_chains, K, n_steps, f_pos, dst,
                              ctx->stream)))
+    return rc;
+  HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(p, dp, sb, hipMemcpyDeviceToHost, ctx->stream));
+  if (status) HIP_TRY(hipMemcpyAsync(status, dst, tb, hipMemcpyDeviceToHost, ctx->stream));
+  HIP_TRY(hipStreamSynchronize(ctx->stream));
+  return RHMC_OK;
+}
+
+int rhmc_hmc_random_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt,
+                           double* d_q, double* d_p, const int32_t* d_steps, int64_t n_chains,
+                           int32_t K, int32_t* d_status, void* stream) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains > 0 && (!d_q || !d_p)) return fail(RHMC_ERR_ARG, "q/p is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_hmc_random(ctx, P, d_dt, d_q, d_p, d_steps, n_chains, K, d_status, s);
+}
+
+int rhmc_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* dt, double* q, double* p,
+                    const int32_t* steps, int64_t n_chains, int32_t K, int32_t* status) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0) return RHMC_OK;
+  if (!q || !p || !dt || !steps) return fail(RHMC_ERR_ARG, "q/p/dt/steps is NULL");
+  for (int64_t i = 0; i < n_chains; ++i)
+    if (steps[i] < 1) return fail(RHMC_ERR_ARG, "steps[i] must be >= 1");
+  const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
+  const size_t tb = (size_t)n_chains * sizeof(int32_t);
+  const size_t db = (size_t)3 * K * sizeof(double);
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  HIP_TRY(hipSetDevice(ctx->device));
+  if ((rc = ensure_scratch(ctx, 2 * up(sb) + 2 * up(tb) + up(db)))) return rc;
+  char* base = (char*)ctx->scratch;
+  double* dq = (double*)base;
+  double* dp = (double*)(base + up(sb));
+  int32_t* dst = (int32_t*)(base + 2 * up(sb));
+  int32_t* dsteps = (int32_t*)(base + 2 * up(sb) + up(tb));
+  double* ddt = (double*)(base + 2 * up(sb) + 2 * up(tb));
+  HIP_TRY(hipMemcpyAsync(dq, q, sb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dp, p, sb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(dsteps, steps, tb, hipMemcpyHostToDevice, ctx->stream));
+  HIP_TRY(hipMemcpyAsync(ddt, dt, db, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = launch_hmc_random(ctx, P, ddt, dq, dp, dsteps, n_chains, K, dst, ctx->stream)))
     return rc;
   HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
   HIP_TRY(hipMemcpyAsync(p, dp, sb, hipMemcpyDeviceToHost, ctx->stream));

@@ -32,7 +32,11 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
            "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
            "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
-           "rhmc_gen_image", "rhmc_gen_image_device")
+           "rhmc_gen_image", "rhmc_gen_image_device", "rhmc_hmc_random",
+           "rhmc_hmc_random_device")
+
+V_FLUX_WALL = 1       # rhmc_energy f_pos bits (include/rhmc.h)
+V_NO_POSCHECK = 2
 
 SOLVER_IMPLICIT = 0
 SOLVER_HMC = 1
@@ -110,6 +114,10 @@ def _load():
         "rhmc_mh_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                           ctypes.c_uint64, P(MhRecord), vp]),
+        "rhmc_hmc_random": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_ip,
+                                           ctypes.c_int64, ctypes.c_int32, c_ip]),
+        "rhmc_hmc_random_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, vp, vp,
+                                                  ctypes.c_int64, ctypes.c_int32, vp, vp]),
         "rhmc_gen_image": (ctypes.c_int, [vp, P(RhmcParams), c_dp, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_uint64, c_dp,
                                           ctypes.c_int32]),
@@ -265,8 +273,9 @@ class Context:
                                   q2.shape[0], q2.shape[1] // 3, int(kind)))
         return g[0] if single else g
 
-    def energy(self, params, q, p=None, f_pos=False):
-        """Returns (V, T); T is None when p is None."""
+    def energy(self, params, q, p=None, f_pos=False, pos_check=True):
+        """Returns (V, T); T is None when p is None.  pos_check=False drops the
+        position support check (samplers.lightsource_gym.V has none)."""
         q2 = np.array(q, dtype=np.float64, order="C", copy=True)
         single = q2.ndim == 1
         q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
@@ -280,7 +289,7 @@ class Context:
         _check(_lib.rhmc_energy(self._h, ctypes.byref(params), _dptr(q2),
                                 None if pp is None else _dptr(pp), _dptr(V),
                                 None if T is None else _dptr(T), n, q2.shape[1] // 3,
-                                int(bool(f_pos))))
+                                (V_FLUX_WALL if f_pos else 0) | (0 if pos_check else V_NO_POSCHECK)))
         if single:
             return V[0], (None if T is None else T[0])
         return V, T
@@ -348,6 +357,26 @@ class Context:
                                           int(n_chains), int(K), int(n_steps),
                                           int(bool(f_pos)), ctypes.c_void_p(status_ptr or 0),
                                           ctypes.c_void_p(stream or 0)))
+
+    def hmc_random(self, params, dt, q, p, steps, return_status=False):
+        """samplers.HMC_random trajectories (rhmc_hmc_random): per-coordinate
+        step vector dt [3K], steps[c] >= 1 leapfrog steps for chain c, flux
+        wall at params.f_lim.  Returns new (q, p) (p is the input momentum on
+        chains whose last step flipped — the reference's stale-p quirk)."""
+        q2 = np.array(q, dtype=np.float64, order="C", copy=True)
+        p2 = np.array(p, dtype=np.float64, order="C", copy=True)
+        single = q2.ndim == 1
+        q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
+        p2 = p2.reshape(q2.shape)
+        K = q2.shape[1] // 3
+        dt2 = np.ascontiguousarray(np.broadcast_to(np.asarray(dt, np.float64), (3 * K,)))
+        st = np.zeros(q2.shape[0], np.int32)
+        n = np.ascontiguousarray(np.broadcast_to(np.asarray(steps, np.int32), (q2.shape[0],)))
+        _check(_lib.rhmc_hmc_random(self._h, ctypes.byref(params), _dptr(dt2), _dptr(q2),
+                                    _dptr(p2), _iptr(n), q2.shape[0], K, _iptr(st)))
+        if single:
+            q2, p2, st = q2[0], p2[0], st[0]
+        return (q2, p2, st) if return_status else (q2, p2)
 
     def gen_image(self, params, q, rows, cols, n_real=0, seed=0, install=False):
         """Model image (n_real=0, gen_model) or n_real Poisson realisations of it

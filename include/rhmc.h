@@ -150,8 +150,14 @@ int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
 int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
                   double* grad, int64_t n_chains, int32_t K, int32_t kind);
 
-/* V (:294-351, with f_pos) and T at H(q) (:353-363) per chain.  V or T may
- * be NULL.  p may be NULL when T is NULL.  Host pointers. */
+/* V (:294-351) and T at H(q) (:353-363) per chain.  V or T may be NULL.  p
+ * may be NULL when T is NULL.  Host pointers.  f_pos is a bit set:
+ * RHMC_V_FLUX_WALL (1) = V is inf when a flux is below f_lim (:303-309, the
+ * reference's f_pos=True); RHMC_V_NO_POSCHECK (2) = skip the position support
+ * check (:311-317), i.e. samplers.lightsource_gym.V (samplers.py:1137-1150),
+ * which has none. */
+#define RHMC_V_FLUX_WALL   1
+#define RHMC_V_NO_POSCHECK 2
 int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
                 const double* p, double* V, double* T, int64_t n_chains,
                 int32_t K, int32_t f_pos);
@@ -165,6 +171,20 @@ int rhmc_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* 
 int rhmc_integrate_device(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* d_q,
                           double* d_p, int64_t n_chains, int32_t K, int32_t n_steps,
                           int32_t f_pos, int32_t* d_status, void* stream);
+
+/* samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552;
+ * the MH bookkeeping around it, :489-568, stays on the host): unit-mass
+ * leapfrog with the per-coordinate step vector dt[3K] (the reference's
+ * self.dt) and steps[c] >= 1 steps for chain c (its np.random.randint draw),
+ * flux wall at P->f_lim with the reference's quirks (sticky flip mask; when
+ * the last step flipped, p is left at its input value and the chain's status
+ * gets RHMC_STATUS_REFLECT_F).  q, p host [n_chains][3K] updated in place;
+ * status nullable.  Gradient: dVdq without metric (:1108-1135). */
+int rhmc_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* dt, double* q, double* p,
+                    const int32_t* steps, int64_t n_chains, int32_t K, int32_t* status);
+int rhmc_hmc_random_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt,
+                           double* d_q, double* d_p, const int32_t* d_steps, int64_t n_chains,
+                           int32_t K, int32_t* d_status, void* stream);
 
 /* Per-iteration records of rhmc_mh (all nullable; host pointers for rhmc_mh,
  * device pointers for rhmc_mh_device).  Row l holds the state at the START

@@ -53,7 +53,8 @@ def load_reference(ref_dir):
     sys.path.insert(0, tmp)
     import sampler_RHMC  # noqa: E402
     import utils         # noqa: E402
-    return sampler_RHMC, utils, tmp
+    import samplers      # noqa: E402
+    return sampler_RHMC, utils, samplers, tmp
 
 
 class Counter:
@@ -483,12 +484,48 @@ def case_datagen(S, U):
     return out
 
 
+def case_hmc_random(S, U, L):
+    """samplers.lightsource_gym.HMC_random (samplers.py:460-572): the older
+    sampler API's unit-mass HMC with a per-coordinate dt vector, random
+    trajectory lengths and the flux wall (with its sticky-iflip / stale-p
+    quirks, exercised by the "wall" cases).  The global NumPy RNG is seeded
+    right before the call, so a test can replay the draws."""
+    out = {}
+    for name, n, stars_t, stars_m, dt3, niter, smin, smax, f_lim in [
+        ("k1", 16, [[1500., 8.3, 7.9]], [[1400., 8.6, 7.7]], (8.0, 0.08, 0.08), 40, 5, 15, 0.),
+        ("k2", 24, [[2500., 9.3, 10.9], [900., 14.2, 12.1]],
+         [[2400., 9.6, 10.7], [1000., 14.0, 12.4]], (8.0, 0.06, 0.06), 30, 8, 20, 0.),
+        ("wall", 16, [[60., 8.3, 7.9]], [[45., 8.6, 7.7]], (6., 0.05, 0.05), 40, 5, 15, 40.),
+        ("wall2", 20, [[70., 6.3, 7.9], [1800., 12.2, 11.1]],
+         [[48., 6.6, 7.7], [1750., 12.0, 11.4]], (8., 0.05, 0.05), 40, 4, 12, 44.),
+    ]:
+        g = L.lightsource_gym()
+        g.num_rows = g.num_cols = n
+        np.random.seed(77)
+        g.gen_mock_data(np.array(stars_t))
+        K = len(stars_m)
+        g.Nobjs = K
+        g.d = 3 * K
+        g.dt = np.tile(np.array(dt3, dtype=float), K)
+        q0 = np.array(stars_m, dtype=float)
+        np.random.seed(5)
+        with contextlib.redirect_stdout(io.StringIO()):
+            g.HMC_random(q_model_0=q0, Nchain=1, Niter=niter, steps_min=smin,
+                         steps_max=smax, f_lim=f_lim)
+        out.update(pack(name + "/", dict(
+            D=g.D, dt=g.dt, q0=q0.reshape(-1), Niter=niter, steps_min=smin, steps_max=smax,
+            f_lim=f_lim, seed=5, q_chain=g.q_chain[0], E_chain=g.E_chain[0],
+            dE_chain=g.dE_chain[0], A_chain=g.A_chain[0], B_count=g.B_count,
+            fwhm_pix=g.PSF_FWHM_pix)))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
-    S, U, tmp = load_reference(args.ref)
+    S, U, L, tmp = load_reference(args.ref)
     try:
         jobs = {"functions": case_functions, "steps": case_steps,
                 "mh": case_mh, "solvers": case_solvers,
@@ -498,6 +535,9 @@ def main():
                 continue
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **fn(S, U))
             print("wrote", name)
+        if not args.only or args.only == "hmc_random":
+            np.savez_compressed(os.path.join(HERE, "hmc_random.npz"), **case_hmc_random(S, U, L))
+            print("wrote hmc_random")
         if not args.only or args.only == "trajs":
             for name, d in case_trajs(S, U).items():
                 np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)

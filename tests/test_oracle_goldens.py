@@ -107,3 +107,32 @@ def test_model_image(name):
     got = R.model_image(int(par["rows"]), int(par["cols"]), z[name + "/q"], par["B_count"],
                         par["fwhm_pix"])
     np.testing.assert_array_equal(got, z[name + "/model"])
+
+
+def hmc_random_model(z, name):
+    """Oracle model for a hmc_random golden case (lightsource_gym: no prior,
+    unit metric; only B and the PSF width matter)."""
+    D = z[name + "/D"]
+    n = D.shape[0]
+    par = dict(rows=n, cols=n, B_count=float(z[name + "/B_count"]),
+               fwhm_pix=float(z[name + "/fwhm_pix"]), use_prior=0, use_Vc=0, alpha=2.,
+               beta=1., Vc_r_pow=1., dt=1., f_lim=float(z[name + "/f_lim"]), f_low=1.,
+               g_xx=1., g_ff=1., g_ff2=1., g0=1., g1=1., g2=1., fmin=-1., fmax=-1.)
+    return R.RefModel(D, par)
+
+
+@pytest.mark.parametrize("name", ["k1", "k2", "wall", "wall2"])
+def test_hmc_random_exact(name):
+    """samplers.lightsource_gym.HMC_random (per-coordinate dt, random
+    trajectory lengths, sticky-flip / stale-p flux-wall quirks) replayed from
+    the reference's seed: bit-identical chains, energies and decisions."""
+    z = load_golden("hmc_random")
+    m = hmc_random_model(z, name)
+    rs = np.random.RandomState(int(z[name + "/seed"]))
+    qc, Ec, dEc, Ac = m.hmc_random(z[name + "/q0"], z[name + "/dt"], int(z[name + "/Niter"]),
+                                   int(z[name + "/steps_min"]), int(z[name + "/steps_max"]),
+                                   float(z[name + "/f_lim"]), rng=rs)
+    np.testing.assert_array_equal(qc, z[name + "/q_chain"])
+    np.testing.assert_array_equal(Ec, z[name + "/E_chain"])
+    np.testing.assert_array_equal(dEc, z[name + "/dE_chain"])
+    np.testing.assert_array_equal(Ac, z[name + "/A_chain"])
