@@ -19,14 +19,13 @@ changed later; single_gym ignores its g_ff2 argument; V needs fmin/fmax for
 its prior constant (computed and cached on the first V call); use_Vc needs
 f_expnt to be set (TypeError otherwise, like the reference).
 
-Out of scope here: plotting (display_image, diagnostics_*) and
-the reversible-jump birth/death/split/merge moves (P_move[1:] must be 0).
+Out of scope here: plotting (display_image, diagnostics_*).
 """
 import numpy as np
 
 from . import capi
-from .photometry import (default_exp_setup, factors, flux2mag, gauss_PSF, mag2flux,
-                         poisson_realization)
+from .photometry import (default_exp_setup, factors, flux2mag, gauss_PSF,
+                         gen_pow_law_sample, mag2flux, poisson_realization)
 
 
 class base_class(object):
@@ -417,14 +416,14 @@ class multi_gym(base_class):
     def run_RHMC(self, q_model_0, f_pos=True, delta=1e-6, Niter=100, Nsteps=100, dt=1e-1,
                  save_traj=False, counter_max=1000, verbose=False, q_true=None,
                  schedule_g_ff2=None, N_max=50, P_move=[1., 0., 0.], schedule_beta=None):
-        """sampler_RHMC.py:937-1198, move-0 ("within") branch.  The Nsteps
-        leapfrog steps of an iteration are ONE fused launch.  Same global
-        NumPy RNG order per iteration as the reference: randn(d), choice
-        (one uniform), random(1)."""
+        """sampler_RHMC.py:937-1198.  Each batch of Nsteps leapfrog steps is ONE
+        fused launch.  Same global NumPy RNG stream as the reference: per
+        iteration randn(d), the move-type choice (one uniform), then for
+        move 0 random(1); for the reversible-jump moves (P_move[1:] != 0) the
+        grow/shrink choice, the move's own draws (birth_death_move /
+        split_merge_move) and random(1)."""
         if save_traj:
             assert False                                  # :966-968
-        if P_move[1] != 0 or P_move[2] != 0:
-            raise NotImplementedError("reversible-jump moves are out of scope (P_move[1:] != 0)")
         self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
         self.save_traj, self.P_move, self.N_max = save_traj, P_move, N_max
         self.Nobjs = q_model_0.shape[0]
@@ -456,16 +455,41 @@ class multi_gym(base_class):
             self.T_chain[l] = T_initial
             self.N_chain[l] = self.Nobjs
             move_type = np.random.choice([0, 1, 2], p=self.P_move, size=1)[0]
-            self.move_chain[l] = 0
+            if move_type == 0:                            # :1048-1088
+                self.move_chain[l] = 0
+                q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
+                                               counter_max=counter_max)
+                H_diag = self.H(q_tmp, grad=False)
+                E_final = self.V(q_tmp, f_pos=f_pos) + self.T(p_tmp, H_diag)
+                dE = E_final - E_initial
+                lnu = np.log(np.random.random(1))
+                if (dE < 0) or (lnu < -dE):
+                    self.A_chain[l] = 1
+                else:
+                    q_tmp = self.q_chain[l, :self.d]
+                continue
+            # reversible-jump moves (:1089-1187): Nsteps RHMC steps, momentum
+            # flip, the dimension-changing proposal, Nsteps steps, flip, then
+            # accept with ln alpha0 = -dE + factor
+            grow = np.random.choice([True, False], p=[0.5, 0.5])
+            self.move_chain[l] = (1 if grow else 2) if move_type == 1 else (3 if grow else 4)
             q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
                                            counter_max=counter_max)
+            p_tmp = -p_tmp
+            move = self.birth_death_move if move_type == 1 else self.split_merge_move
+            q_tmp, p_tmp, factor = move(q_tmp, p_tmp, grow)
+            q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
+                                           counter_max=counter_max)
+            p_tmp = -p_tmp
             H_diag = self.H(q_tmp, grad=False)
             E_final = self.V(q_tmp, f_pos=f_pos) + self.T(p_tmp, H_diag)
-            dE = E_final - E_initial
+            ln_alpha0 = -(E_final - E_initial) + factor
             lnu = np.log(np.random.random(1))
-            if (dE < 0) or (lnu < -dE):
+            if (ln_alpha0 > 0) or (lnu < ln_alpha0):
                 self.A_chain[l] = 1
-            else:
+            else:                                         # undo the dimension change
+                self.Nobjs += -1 if grow else 1
+                self.d = 3 * self.Nobjs
                 q_tmp = self.q_chain[l, :self.d]
             if verbose and (l % 50) == 0:
                 print("/---- Completed iteration %d" % l)
@@ -473,6 +497,110 @@ class multi_gym(base_class):
                 self.R_accept_report(idx_iter=l, run_window=10)
         print("Finished. Final report.")                  # :1195-1196
         self.R_accept_report(idx_iter=-1, running=False)
+
+    # ------------------------------------------------ reversible-jump moves
+    def _one_star_T(self, q3, p3):
+        """T of a single star (q3, p3 of length 3) at its own metric."""
+        H3 = self.H(q3, grad=False)
+        return self.T(p3, H3), H3
+
+    def birth_death_move(self, q_tmp, p_tmp, birth_death=None):
+        """sampler_RHMC.py:1200-1270.  Birth (True): a new star with x, y
+        uniform on [1, n-1), flux from the power-law prior, momentum from its
+        own metric, appended last.  Death (False): a uniformly chosen star is
+        removed.  Returns (q, p, ln-acceptance correction); updates Nobjs, d."""
+        if birth_death is None or self.alpha is None or self.fmin is None or self.fmax is None:
+            assert False                                  # :1205-1207 (prior required)
+        if birth_death:
+            x = np.random.random() * (self.num_rows - 2.) + 1.
+            y = np.random.random() * (self.num_cols - 2.) + 1.
+            f = gen_pow_law_sample(self.alpha, self.fmin, self.fmax, 1)[0]
+            q_new = np.array([f, x, y])
+            H3 = self.H(q_new, grad=False)
+            p_new = self.u_sample(3) * np.sqrt(H3)
+            q = np.concatenate([q_tmp, q_new])
+            p = np.concatenate([p_tmp, p_new])
+            factor = (self.alpha * np.log(f) - 3 / 2. + self.T(p_new, H3)
+                      + self.V_prior_const)
+            self.Nobjs += 1
+        else:
+            k = np.random.randint(0, self.Nobjs, size=1)[0]
+            sl = slice(3 * k, 3 * k + 3)
+            T_k, _ = self._one_star_T(q_tmp[sl], p_tmp[sl])
+            factor = -self.alpha * np.log(q_tmp[3 * k]) + 3 / 2. - T_k - self.V_prior_const
+            q = np.delete(q_tmp, np.s_[sl])
+            p = np.delete(p_tmp, np.s_[sl])
+            self.Nobjs -= 1
+        self.d = 3 * self.Nobjs
+        return q, p, factor
+
+    def split_merge_move(self, q_tmp, p_tmp, split_merge=None):
+        """sampler_RHMC.py:1273-1445.  Split (True): star i (uniform) becomes
+        (F f, x + (1-F) dx, y + (1-F) dy) in place and ((1-F) f, x - F dx,
+        y - F dy) appended, F ~ Beta(beta_a, beta_b), (dx, dy) ~ N(0,
+        K_split^2); fresh momenta for both.  Merge (False): a pair (i, j)
+        chosen with probability ~ Beta(F_ij) N(r_ij) (self-pairs excluded),
+        removed, and the flux-weighted merged star appended with a fresh
+        momentum.  Returns (q, p, ln-acceptance correction)."""
+        from scipy.stats import beta as BETA
+        if split_merge is None:
+            assert False
+        a, b, Ks = self.beta_a, self.beta_b, self.K_split
+        ln_q_dxdy = np.log(2 * np.pi * Ks ** 2)
+        if split_merge:
+            i = np.random.randint(0, self.Nobjs, size=1)[0]
+            f_s, x_s, y_s = q_tmp[3 * i:3 * i + 3]
+            q_star = np.copy(q_tmp[3 * i:3 * i + 3])
+            p_star = np.copy(p_tmp[3 * i:3 * i + 3])
+            dx, dy = np.random.randn(2) * Ks
+            dr_sq = dx ** 2 + dy ** 2
+            F = BETA.rvs(a, b, size=1)[0]
+            q_1 = np.array([F * f_s, x_s + (1 - F) * dx, y_s + (1 - F) * dy])
+            q_2 = np.array([(1 - F) * f_s, x_s - F * dx, y_s - F * dy])
+            H1 = self.H(q_1, grad=False)
+            p_1 = self.u_sample(3) * np.sqrt(H1)
+            H2 = self.H(q_2, grad=False)
+            p_2 = self.u_sample(3) * np.sqrt(H2)
+            T_star, _ = self._one_star_T(q_star, p_star)
+            q = np.concatenate([q_tmp, q_2])
+            p = np.concatenate([p_tmp, p_2])
+            q[3 * i:3 * i + 3] = q_1
+            p[3 * i:3 * i + 3] = p_1
+            factor = ((-3 / 2.) + np.log(f_s) - BETA.logpdf(F, a, b) + ln_q_dxdy
+                      + (dr_sq / (2 * Ks ** 2)) + self.T(p_1, H1) + self.T(p_2, H2) - T_star)
+            self.Nobjs += 1
+        else:
+            n = self.Nobjs
+            f_v, x_v, y_v = q_tmp[0::3][:n], q_tmp[1::3][:n], q_tmp[2::3][:n]
+            F_m = f_v / (f_v.reshape((n, 1)) + f_v)
+            P = BETA.pdf(F_m, a, b)
+            P[np.abs(F_m - 0.5) < 1e-6] = 0.              # no self-merging
+            R_sq = (x_v.reshape((n, 1)) - x_v) ** 2 + (y_v.reshape((n, 1)) - y_v) ** 2
+            P = P * (np.exp(-R_sq / (2. * Ks ** 2)) / (2. * np.pi * Ks ** 2))
+            P /= np.sum(P)
+            pair = np.random.choice(range(n ** 2), p=P.ravel())
+            i1, i2 = pair // n, pair % n
+            q_1, p_1 = np.copy(q_tmp[3 * i1:3 * i1 + 3]), np.copy(p_tmp[3 * i1:3 * i1 + 3])
+            q_2, p_2 = np.copy(q_tmp[3 * i2:3 * i2 + 3]), np.copy(p_tmp[3 * i2:3 * i2 + 3])
+            F = q_1[0] / (q_1[0] + q_2[0])
+            dx, dy = q_1[1] - q_2[1], q_1[2] - q_2[2]
+            dr_sq = dx ** 2 + dy ** 2
+            q_star = np.array([q_1[0] + q_2[0], F * q_1[1] + (1 - F) * q_2[1],
+                               F * q_1[2] + (1 - F) * q_2[2]])
+            T_1, _ = self._one_star_T(q_1, p_1)
+            T_2, _ = self._one_star_T(q_2, p_2)
+            H_s = self.H(q_star, grad=False)
+            p_star = self.u_sample(3) * np.sqrt(H_s)
+            T_star = self.T(p_star, H_s)
+            lo, hi = min(i1, i2), max(i1, i2)
+            keep = [np.s_[:3 * lo], np.s_[3 * lo + 3:3 * hi], np.s_[3 * hi + 3:]]
+            q = np.concatenate([q_tmp[k] for k in keep] + [q_star])
+            p = np.concatenate([p_tmp[k] for k in keep] + [p_star])
+            factor = ((3 / 2.) - np.log(q_star[0]) + BETA.logpdf(F, a, b) - ln_q_dxdy
+                      - (dr_sq / (2 * Ks ** 2)) - T_1 - T_2 + T_star)
+            self.Nobjs -= 1
+        self.d = 3 * self.Nobjs
+        return q, p, factor
 
     def run_RHMC_batched(self, q_model_0, f_pos=True, delta=1e-6, Niter=100, Nsteps=100,
                          dt=1e-1, counter_max=1000, rng="numpy", seeds=None, seed=0):

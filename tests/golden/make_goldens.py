@@ -520,6 +520,54 @@ def case_hmc_random(S, U, L):
     return out
 
 
+def case_rj(S, U):
+    """multi_gym.run_RHMC with the reversible-jump moves on (P_move[1:] != 0,
+    sampler_RHMC.py:1089-1187; birth_death_move :1200-1270, split_merge_move
+    :1273-1445, scipy Beta for the split fraction).  A seed whose run hits
+    one of the reference's own dead ends (no star left, nothing mergeable) is
+    skipped; the seed used is recorded."""
+    out = {}
+    for name, stars_t, stars_m, P_move, niter, nsteps, seeds in [
+        ("rj_bd", [[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4]], [0.4, 0.6, 0.], 40, 8, range(100, 140)),
+        ("rj_sm", [[18., 10.2, 12.7], [19., 20.3, 18.1], [19.5, 11., 14.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4]], [0.4, 0., 0.6], 40, 8, range(200, 240)),
+        ("rj_all", [[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4], [19.6, 15.3, 24.6]], [0.4, 0.3, 0.3], 50, 6,
+         range(300, 340)),
+    ]:
+        for seed in seeds:
+            np.random.seed(77)
+            g = make_gym(S, n=32, g_xx=0.05, g_ff=4., g_ff2=4., prior=True)
+            g.gen_mock_data(np.array(stars_t))
+            np.random.seed(seed)
+            try:
+                with contextlib.redirect_stdout(io.StringIO()), np.errstate(all="ignore"):
+                    g.run_RHMC(np.array(stars_m), f_pos=True, delta=1e-6, Niter=niter,
+                               Nsteps=nsteps, dt=0.05, N_max=8, P_move=P_move)
+            except Exception:
+                continue
+            moves = np.bincount(g.move_chain, minlength=5)
+            acc = np.bincount(g.move_chain[g.A_chain], minlength=5)
+            if (P_move[1] > 0 and (acc[1] == 0 or acc[2] == 0 and moves[2] == 0)) or \
+               (P_move[2] > 0 and (moves[3] == 0 or moves[4] == 0)):
+                continue          # want every move type proposed (and some jumps accepted)
+            break
+        else:
+            raise RuntimeError("no usable seed for " + name)
+        res = dict(D=g.D, q_model=np.array(stars_m), q_chain=g.q_chain, p_chain=g.p_chain,
+                   E_chain=g.E_chain, V_chain=g.V_chain, T_chain=g.T_chain,
+                   A_chain=g.A_chain.astype(np.int32), move_chain=g.move_chain,
+                   N_chain=g.N_chain, P_move=np.array(P_move), niter=niter, nsteps=nsteps,
+                   seed=seed, dt=0.05, N_max=8)
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+        print(name, "seed", seed, "moves", np.bincount(g.move_chain, minlength=5),
+              "accepted", np.bincount(g.move_chain[g.A_chain], minlength=5),
+              "N", g.N_chain.min(), g.N_chain.max())
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -535,6 +583,9 @@ def main():
                 continue
             np.savez_compressed(os.path.join(HERE, name + ".npz"), **fn(S, U))
             print("wrote", name)
+        if not args.only or args.only == "rj":
+            np.savez_compressed(os.path.join(HERE, "rj.npz"), **case_rj(S, U))
+            print("wrote rj")
         if not args.only or args.only == "hmc_random":
             np.savez_compressed(os.path.join(HERE, "hmc_random.npz"), **case_hmc_random(S, U, L))
             print("wrote hmc_random")

@@ -172,3 +172,28 @@ def test_single_gym_alternative_integrators(gpu_lib, name, solver):
     assert np.array_equal(np.isinf(E), np.isinf(Ew))
     fin = np.isfinite(Ew)
     np.testing.assert_allclose(E[fin], Ew[fin], rtol=1e-9, atol=1e-7)
+
+
+@pytest.mark.parametrize("name", ["rj_bd", "rj_sm", "rj_all"])
+def test_run_RHMC_reversible_jump_moves(gpu_lib, name):
+    """run_RHMC with birth/death and split/merge proposals (sampler_RHMC.py
+    :1089-1187, :1200-1445): the same global-RNG stream (incl. scipy's Beta
+    draws) gives the reference's move types, accept decisions, star counts
+    and chains; the trajectories on both sides of a jump run on the GPU at
+    the changed dimension."""
+    z = load_golden("rj")
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    np.random.seed(int(z[name + "/seed"]))
+    g.run_RHMC(z[name + "/q_model"].copy(), f_pos=True, delta=1e-6,
+               Niter=int(z[name + "/niter"]), Nsteps=int(z[name + "/nsteps"]),
+               dt=float(z[name + "/dt"]), N_max=int(z[name + "/N_max"]),
+               P_move=list(z[name + "/P_move"]))
+    np.testing.assert_array_equal(g.move_chain, z[name + "/move_chain"])
+    np.testing.assert_array_equal(g.N_chain, z[name + "/N_chain"])
+    np.testing.assert_array_equal(g.A_chain.astype(np.int32), z[name + "/A_chain"])
+    assert (g.move_chain[g.A_chain] > 0).any()       # some dimension change accepted
+    assert_state_close(g.q_chain, z[name + "/q_chain"], 1e-9, "q_chain")
+    assert_state_close(g.p_chain, z[name + "/p_chain"], 1e-9, "p_chain")
+    np.testing.assert_allclose(g.E_chain, z[name + "/E_chain"], rtol=1e-11)

@@ -77,8 +77,10 @@ def test_quirk_errors_like_reference():
     g2 = sampler.multi_gym()
     with pytest.raises(TypeError):                # fmin/fmax None -> TypeError (:321)
         g2._params(for_energy=True)
-    with pytest.raises(NotImplementedError):
-        g2.run_RHMC(np.array([[19., 24., 24.]]), P_move=[0.6, 0.2, 0.2])
+    g3 = sampler.multi_gym()
+    g3.fmin = g3.fmax = None
+    with pytest.raises(AssertionError):            # birth needs the prior range (:1205-1207)
+        g3.birth_death_move(np.zeros(3), np.zeros(3), birth_death=True)
 
 
 @pytest.mark.parametrize("name,cls", [("k1_48", "multi"), ("k1_32", "single"),
