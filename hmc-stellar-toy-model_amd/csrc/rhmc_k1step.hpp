@@ -64,7 +64,8 @@ __device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
 
 // n_steps steps on (f, x, y, pf, px, py).  grad(f, x, y, gf, gx, gy) returns
 // the pixel part of dphidq: gf = -sum psf (D/L - 1), gx, gy (:404-406).
-// PROF (tools only): prof[0] += cycles in grad, prof[1] += cycles elsewhere.
+// PROF (tools only): per-phase cycle sums, prof[0] gradient, prof[1] kicks +
+// reflection + p-loop, prof[2] q-loop, prof[3] flux metric + closing update.
 template <bool PROF = false, class GRAD>
 __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double& pf,
                                          double& px, double& py, int n_steps, double edge,
@@ -74,21 +75,24 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
   const double hdt = c.hdt;
   FluxMetric fm = flux_metric(f, c, lc);
   long long t0 = 0;
+  // phase boundary: fenced clock read; the cycles since the last boundary go
+  // to bucket `close` (a constant at every call site)
+  auto mark = [&](int close) {
+    if constexpr (PROF) {
+      __builtin_amdgcn_sched_barrier(0);
+      const long long t1 = clock64();
+      if (t0) prof[close] += t1 - t0;
+      t0 = t1;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
   for (int s = 0;; ++s) {
     double gf, gx, gy;
-    if constexpr (PROF) {
-      const long long t1 = clock64();
-      if (s > 0) prof[1] += t1 - t0;
-      t0 = t1;
-    }
+    mark(3);
     RHMC_MARK(1);
     grad(f, x, y, gf, gx, gy);
     RHMC_MARK(2);
-    if constexpr (PROF) {
-      const long long t1 = clock64();
-      prof[0] += t1 - t0;
-      t0 = t1;
-    }
+    mark(0);
     if (c.use_prior) gf += fm.prior;               // :408-409
     gf += fm.mterm;                                // :459-463
     if (s > 0) {
@@ -108,7 +112,10 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
         st |= RHMC_STATUS_REFLECT_XY;
       }
     }
-    if (s == n_steps) break;
+    if (s == n_steps) {
+      mark(1);
+      break;
+    }
     pf = pf - hdt * gf;                            // :525
     px = px - hdt * gx;
     py = py - hdt * gy;
@@ -145,6 +152,7 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (more) st |= RHMC_STATUS_PLOOP_CAP;
       RHMC_MARK(3);
     }
+    mark(1);
     {                                              // :538-545
       // q_{n+1} = q_s + hdt (p/H(q_s) + p/H(q_n)) with 1/H_ff(f) = f/g_ff2 + c0
       // and 1/H_xx(f) = g(f)/g_xx, g = u/g1 + (B/g2) u^2: affine in f and g.
@@ -199,6 +207,7 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (more) st |= RHMC_STATUS_QLOOP_CAP;
       RHMC_MARK(4);
     }
+    mark(2);
     fm = flux_metric(f, c, lc);
     pf = pf - hdt * ((pf * pf) * fm.coef / 2.0);   // :548
     RHMC_MARK(5);

@@ -285,16 +285,18 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
   TL::init(cache);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  long long prof[2] = {0, 0};
+  long long prof[4] = {0, 0, 0, 0};
   k1_steps<PROF>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
                  [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
                    TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
                  },
                  it_p, it_q, st, prof);
-  if constexpr (PROF) {
-    const int ns = a.n_steps > 0 ? a.n_steps : 1;
-    it_p = (int)(prof[0] / ns);
-    it_q = (int)(prof[1] / ns);
+  if constexpr (PROF) {  // tools only: cycles per step per phase replace the state
+    const double ns = a.n_steps > 0 ? a.n_steps : 1;
+    f = prof[0] / ns;
+    x = prof[1] / ns;
+    y = prof[2] / ns;
+    pf = prof[3] / ns;
   }
 
   if ((lane % TL::LPC) == 0 && real) {

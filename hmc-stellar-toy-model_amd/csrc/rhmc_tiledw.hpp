@@ -160,7 +160,7 @@ leapfrog_k1_tiledw(LeapArgsK1 a) {
   const LeanConsts lc = lean_consts(c);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  long long prof[2] = {0, 0};
+  long long prof[4] = {0, 0, 0, 0};
   k1_steps<PROF>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
                  [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
                    TL::gradient(lds, tab, f_, x_, y_, c, lc, gf, gx, gy);
@@ -169,7 +169,7 @@ leapfrog_k1_tiledw(LeapArgsK1 a) {
   if constexpr (PROF) {
     const int ns = a.n_steps > 0 ? a.n_steps : 1;
     it_p = (int)(prof[0] / ns);
-    it_q = (int)(prof[1] / ns);
+    it_q = (int)((prof[1] + prof[2] + prof[3]) / ns);
   }
 
   if ((lane % LPC) == 0 && real) {

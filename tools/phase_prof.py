@@ -1,30 +1,43 @@
 #!/usr/bin/env python3
-"""Per-phase cycle split of the single-star kernel (RHMC_KERNEL=profw16|profw32):
-table build, pixel loop + reductions, fixed-point loops; cycles per step per wave."""
-import os, sys
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "hmc-stellar-toy-model_amd"))
-import numpy as np
-import torch
-from rhmc_amd import capi, workloads
+"""Per-phase cycle split of the single-star kernels (tools only).
+
+RHMC_KERNEL=profr  register-window kernel: cycles per step per wave in the
+                   gradient, kicks + reflection + p-loop, q-loop, and flux
+                   metric + closing update (fenced s_memtime reads; the PROF
+                   build writes them over the chain state).
+RHMC_KERNEL=profw16|profw32  LDS-window kernel: gradient vs the rest.
+usage: RHMC_KERNEL=profr python tools/phase_prof.py [n_chains]
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                "hmc-stellar-toy-model_amd"))
+import torch  # noqa: E402
+
+from rhmc_amd import capi, workloads  # noqa: E402
+
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+kern = os.environ.get("RHMC_KERNEL", "")
 wl = workloads.make("C2", n_chains=n)
 P = capi.make_params(**wl.params)
 ctx = capi.Context(wl.D)
 dev = torch.device("cuda", 0)
-q = torch.from_numpy(wl.q0).to(dev).contiguous()
-p = torch.from_numpy(wl.p0).to(dev).contiguous()
 it = torch.zeros((n, 2), dtype=torch.int32, device=dev)
 st = torch.zeros(n, dtype=torch.int32, device=dev)
 s = torch.cuda.Stream(dev)
 for _ in range(2):
-    ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), n, 1, 200, it.data_ptr(), st.data_ptr(), s.cuda_stream)
+    q = torch.from_numpy(wl.q0).to(dev).contiguous()
+    p = torch.from_numpy(wl.p0).to(dev).contiguous()
+    ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), n, 1, 200, it.data_ptr(), st.data_ptr(),
+                        s.cuda_stream)
 torch.cuda.synchronize()
-a = it.cpu().numpy().astype(float)
-b = st.cpu().numpy().astype(float)
-if os.environ.get("RHMC_KERNEL", "").startswith(("profw", "profr")):
-    print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
-        os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), a.sum(1).mean()))
+if kern.startswith("profr"):
+    qq, pp = q.cpu().numpy(), p.cpu().numpy()
+    ph = [qq[:, 0].mean(), qq[:, 1].mean(), qq[:, 2].mean(), pp[:, 0].mean()]
+    print("%s n=%d cycles/step: gradient %.0f  kicks+p-loop %.0f  q-loop %.0f  flux+tail %.0f"
+          "  total %.0f" % (kern, n, ph[0], ph[1], ph[2], ph[3], sum(ph)))
 else:
-    tot = a[:, 0] + a[:, 1] + b
-    print("%s n=%d cycles/step: table %.0f  pixel+reduce %.0f  loops %.0f  total %.0f" % (
-        os.environ.get("RHMC_KERNEL"), n, a[:, 0].mean(), a[:, 1].mean(), b.mean(), tot.mean()))
+    a = it.cpu().numpy().astype(float)
+    print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
+        kern, n, a[:, 0].mean(), a[:, 1].mean(), a.sum(1).mean()))
