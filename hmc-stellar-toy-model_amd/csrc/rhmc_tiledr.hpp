@@ -64,16 +64,24 @@ constexpr int kRcpGroup = RHMC_RCP_GROUP;
 
 // DT: the type the window pixels are cached in (float when the image is
 // exactly representable in fp32, else double).
-template <int IMG, int WIN, typename DT>
+//
+// ROW0 / TR select a row slice of the window for this wave: lane row a owns
+// window rows ROW0 + a TR .. + TR - 1 (the whole window: ROW0 = 0, TR = WIN/4).
+// A two-wave split (rows 0-11 with the serial step on one wave, rows 12-27 on
+// a helper wave, two workgroup barriers per step) was measured at 0.8x of the
+// single-wave kernel at 4096 chains and dropped.
+template <int IMG, int WIN, typename DT, int ROW0 = 0, int TR_ = WIN / 4>
 struct TiledR {
   static constexpr int LPC = 16;           // lanes per chain
   static constexpr int CPW = kWave / LPC;  // chains per wave
   static constexpr int P = IMG + 1;        // LDS row pitch
-  static constexpr int TR = WIN / 4;       // window rows per lane
+  static constexpr int TR = TR_;           // window rows per lane
   static constexpr int TC = WIN / 4;       // window columns per lane
   static constexpr int NPX = TR * TC;
+  static constexpr int NTR = (TR + 3) / 4; // row factors evaluated per lane
   static_assert(WIN == 28 || WIN == 32, "window side");
   static_assert(IMG >= WIN, "window inside the image");
+  static_assert(ROW0 + 4 * TR <= WIN && TR <= 8, "row slice inside the window");
 
   // LDS: the exp table (64 doubles), then the image as DT [IMG][P].
   static __host__ __device__ constexpr size_t lds_bytes() {
@@ -129,18 +137,20 @@ struct TiledR {
     return swizzle_d<0x13 | ((J << 2) << 5)>(v);
   }
 
-  // Pixel part of the chain's dphidq (every lane of the chain gets it).
-  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
-                                                  const DT* __restrict__ sD, Cache& k,
-                                                  double f, double x, double y, const Consts& c,
-                                                  const LeanConsts& lc, double& gf, double& gx,
-                                                  double& gy) {
+  // The row slice's sums of the chain's dphidq pixel terms: s0 = sum psf s,
+  // s1 = sum psf s dx, s2 = sum psf s dy (s = D/Lambda - 1; every lane of the
+  // chain gets them).
+  static __device__ __forceinline__ void partial(const double* __restrict__ etab,
+                                                 const DT* __restrict__ sD, Cache& k, double f,
+                                                 double x, double y, const Consts& c,
+                                                 const LeanConsts& lc, double& s0, double& s1,
+                                                 double& s2) {
     const int m = lane_id() % LPC;
     const int a = m / 4, b = m % 4;
     const bool stay = x >= k.xlo && x < k.xhi && y >= k.ylo && y < k.yhi;
     if (__builtin_amdgcn_ballot_w64(!stay) != 0) {
       const int r0 = origin(x), c0 = origin(y);
-      const DT* base = sD + (r0 + TR * a) * P + c0 + b;
+      const DT* base = sD + (r0 + ROW0 + TR * a) * P + c0 + b;
 #pragma unroll
       for (int i = 0; i < TR; ++i)
 #pragma unroll
@@ -151,13 +161,15 @@ struct TiledR {
       bounds(y, k.ylo, k.yhi);
     }
     const double r0 = k.r0, c0 = k.c0;
-    // PSF factors: 2 rows + 2 columns per lane, then broadcast.
-    double rv[2], cv[2];
+    // PSF factors: NTR rows + 2 columns per lane, then broadcast.
+    double rv[2] = {0.0, 0.0}, cv[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      const double er = (double)(TR * a + b + 4 * t) + 0.5;  // exact: (r0 + e) + 0.5
-      const double vr = (r0 + er) - x;
-      rv[t] = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
+      if (t < NTR) {
+        const double er = (double)(ROW0 + TR * a + b + 4 * t) + 0.5;  // exact: (r0 + e) + .5
+        const double vr = (r0 + er) - x;
+        rv[t] = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
+      }
       const double ec = (double)(b + 4 * (a + 4 * t)) + 0.5;
       const double vc = (c0 + ec) - y;
       cv[t] = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
@@ -241,11 +253,22 @@ struct TiledR {
       w0 += w;
       w1 = fma(w, (double)(4 * j), w1);
     }
-    const double dxa = ((r0 + (double)(TR * a)) - x) + 0.5;  // offset of the lane's row 0
-    const double dyb = ((c0 + (double)b) - y) + 0.5;         // offset of the lane's column 0
-    const double s0 = group_sum(a0);
-    const double s1 = group_sum(fma(dxa, a0, a1));
-    const double s2 = group_sum(fma(dyb, w0, w1));
+    const double dxa = ((r0 + (double)(ROW0 + TR * a)) - x) + 0.5;  // lane's row 0 offset
+    const double dyb = ((c0 + (double)b) - y) + 0.5;                // lane's column 0 offset
+    s0 = group_sum(a0);
+    s1 = group_sum(fma(dxa, a0, a1));
+    s2 = group_sum(fma(dyb, w0, w1));
+  }
+
+  // Pixel part of the chain's dphidq over the slice (the whole window for the
+  // default slice).
+  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
+                                                  const DT* __restrict__ sD, Cache& k,
+                                                  double f, double x, double y, const Consts& c,
+                                                  const LeanConsts& lc, double& gf, double& gx,
+                                                  double& gy) {
+    double s0, s1, s2;
+    partial(etab, sD, k, f, x, y, c, lc, s0, s1, s2);
     gf = -s0;                                          // :404
     gx = -s1 * f * lc.inv_var;                         // :405
     gy = -s2 * f * lc.inv_var;                         // :406
