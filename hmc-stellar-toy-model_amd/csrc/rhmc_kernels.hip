@@ -33,6 +33,7 @@
 #include "rhmc_tiled2.hpp"
 #include "rhmc_tiledk.hpp"
 #include "rhmc_tiledr.hpp"
+#include "rhmc_tiledrk.hpp"
 #include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -1114,6 +1115,47 @@ int dispatch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
   return launch_tiledk<IMG, 16>(ctx, a, s);
 }
 
+// Multi-star register-window kernel (rhmc_tiledrk.hpp): K in [2, 64], square
+// image of side >= 32, PSF narrow enough for the 28-row window.
+bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c) {
+  return K >= 2 && K <= 64 && ctx->rows == ctx->cols && ctx->rows >= 32 &&
+         reg_window_ok(28, c.inv_two_sig2);
+}
+
+// Which multi-star kernel serves (K, image) by default: the full-image tiled
+// kernel (rhmc_tiledk.hpp) on 32x32 / 48x48 images with K <= 16, where every
+// star's window covers most of the image (C3: 20.1 vs 22.5 ms per 100 steps),
+// the register-window kernel elsewhere (C5: 3.2x the windowed kernel).
+// RHMC_KERNEL=tiledrk / tiledk / windowed / generic force a family.
+bool use_tiledrk(const rhmc_ctx* ctx, int K, const Consts& c) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  if (e && (std::strcmp(e, "tiledk") == 0 || std::strcmp(e, "windowed") == 0 ||
+            std::strcmp(e, "generic") == 0))
+    return false;
+  if (!tiledrk_ok(ctx, K, c)) return false;
+  if (e && std::strcmp(e, "tiledrk") == 0) return true;
+  return !((ctx->rows == 32 || ctx->rows == 48) && K <= kMaxKGeneric);
+}
+
+template <typename DT, int SLOTS>
+int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, hipStream_t s) {
+  using TK = TiledRK<DT, SLOTS>;
+  constexpr int W = 4;
+  const size_t lds = TK::lds_bytes(W);
+  const int64_t waves = (a.n_chains + TK::CPW - 1) / TK::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
+int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
+  const bool f32 = ctx->img_f32;
+  if (f32) a.Df = ctx->d_Df;
+  if (a.K <= 32) return f32 ? launch_kr_t<float, 1>(ctx, a, s) : launch_kr_t<double, 1>(ctx, a, s);
+  return f32 ? launch_kr_t<float, 2>(ctx, a, s) : launch_kr_t<double, 2>(ctx, a, s);
+}
+
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s) {
@@ -1172,6 +1214,22 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
       case 48: return launch_tiled<48>(ctx, t, s);
       default: return launch_tiled<64>(ctx, t, s);
     }
+  }
+  if (use_tiledrk(ctx, K, a.c)) {
+    LeapArgsKR t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = d_it;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n_chains;
+    t.K = K;
+    t.n_steps = n_steps;
+    t.side = ctx->rows;
+    t.pad = 0;
+    t.c = a.c;
+    return launch_kr(ctx, t, s);
   }
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;

@@ -1,0 +1,468 @@
+// rhmc_tiledrk.hpp — multi-star leapfrog (2 <= K <= 64, square images of side
+// >= 32) on per-star pixel windows held in registers: 32 lanes per chain, two
+// chains per wave64.  The many-star counterpart of rhmc_tiledr.hpp (C5:
+// 256x256, K = 64; C3: 48x48, K = 10).
+//
+// Window.  Star k's window is 28 rows x 32 columns: rows
+// floor(x + 0.5) - 14 .., columns floor(y + 0.5) - 16 .. (clamped into the
+// image).  Every pixel left out is >= 14 px (rows) / 16 px (columns) from the
+// star, where PSF/peak <= exp(-14^2 / (2 sigma^2)) <= 2^-62 — the bound
+// rhmc_tiledr.hpp uses (reg_window_ok(28)): such a term changes neither
+// Lambda (f PSF < half an ulp of B) nor the gradient sums beyond their own
+// rounding.
+//
+// Gradient, star-major.  For star k (wave-uniform loop) every lane of a chain
+// owns 28 pixels of k's window: lane m = 8 a + b owns rows 7 a .. 7 a + 6 and
+// columns b, b + 8, b + 16, b + 24.  Lambda at those pixels sums B, star k and
+// every star whose own window overlaps k's window (sampler_RHMC.py:373-376;
+// any other star is outside its window on all of them, so its term is below
+// half an ulp of B); the overlap mask is the union over the wave's two chains
+// (a ballot), so a star counted for one chain only is still exact for the
+// other.  PSF factors are separable (utils.py:475-486): lane (a, b) evaluates
+// the row 7 a + b and the column b + 8 a factor — two exps per star — and
+// ds_swizzle hands them round its row group / column group.  Then
+// s = D/Lambda - 1 with one v_rcp_f64 per pixel pair, the separable row and
+// column sums of rhmc_tiledr.hpp, and three 32-lane all-reduces
+// (:379, :404-406).  The data pixels come from the fp32 copy of D when it is
+// exact (else fp64), L2-resident and shared by every chain.
+//
+// Chain state: lane m holds stars m and m + 32 (SLOTS = 1 or 2) in registers;
+// each gradient reads the chain's (f, x, y) per star from a per-wave LDS table
+// written after every q-loop.  Fixed-point loops (:528-545) run over all the
+// chain's stars at once with np.max's NaN rule via two ballots.
+#pragma once
+#include "rhmc_exp.hpp"
+#include "rhmc_k1step.hpp"
+#include "rhmc_tiled.hpp"
+#include "rhmc_tiled2.hpp"
+#include "rhmc_tiledr.hpp"
+#include "rhmc_wave.hpp"
+
+namespace rhmc {
+
+struct LeapArgsKR {
+  double* q;
+  double* p;
+  int32_t* fp_iters;
+  int32_t* status;
+  const double* D;
+  const float* Df;  // D in fp32 when exact, else nullptr
+  int64_t n_chains;
+  int K, n_steps, side, pad;
+  Consts c;
+};
+
+struct KRStar {  // LDS star table entry
+  double f, x, y, pad;
+};
+
+// This chain's half of a wave ballot (lanes 0-31 or 32-63).
+__device__ __forceinline__ bool half_any(bool v) {
+  const unsigned long long b = __builtin_amdgcn_ballot_w64(v);
+  const unsigned lo = (unsigned)b, hi = (unsigned)(b >> 32);
+  return (lane_id() < 32 ? lo : hi) != 0u;
+}
+
+template <typename DT, int SLOTS>
+struct TiledRK {
+  static constexpr int LPC = 32;           // lanes per chain
+  static constexpr int CPW = kWave / LPC;  // chains per wave
+  static constexpr int KMAX = LPC * SLOTS;
+  static constexpr int WR = 28, WC = 32;   // window rows x columns
+  static constexpr int TR = 7, TC = 4;     // rows x columns per lane
+  static constexpr int NPX = TR * TC;
+  static_assert(SLOTS == 1 || SLOTS == 2, "K <= 64");
+
+  static __host__ __device__ constexpr size_t lds_bytes(int waves) {
+    return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar);
+  }
+  static __device__ __forceinline__ int origin(double v, int half, int omax) {
+    if (!(fabs(v) < 1.0e7)) return 0;
+    const int o = (int)floor(v + 0.5) - half;
+    return o < 0 ? 0 : (o > omax ? omax : o);
+  }
+
+  // PSF factors of a star at (xs, ys) on the window with origin (r0, c0):
+  // ex[t] at row r0 + 7a + t, ey[u] at column c0 + b + 8u (carries 1/(2 pi s^2)).
+  static __device__ __forceinline__ void factors(const double* __restrict__ etab, double r0,
+                                                 double c0, double xs, double ys, int a, int b,
+                                                 const LeanConsts& lc, double (&ex)[TR],
+                                                 double (&ey)[TC]) {
+    const double vr = (r0 + ((double)(7 * a + b) + 0.5)) - xs;  // exact offsets
+    const double er = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
+    const double vc = (c0 + ((double)(b + 8 * a) + 0.5)) - ys;
+    const double ec = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
+    // rows: lane (a, t) of my 8-lane row group; columns: lane (u, b)
+    ex[0] = swizzle_d<0x18 | (0 << 5)>(er);
+    ex[1] = swizzle_d<0x18 | (1 << 5)>(er);
+    ex[2] = swizzle_d<0x18 | (2 << 5)>(er);
+    ex[3] = swizzle_d<0x18 | (3 << 5)>(er);
+    ex[4] = swizzle_d<0x18 | (4 << 5)>(er);
+    ex[5] = swizzle_d<0x18 | (5 << 5)>(er);
+    ex[6] = swizzle_d<0x18 | (6 << 5)>(er);
+    ey[0] = swizzle_d<0x07 | (0 << 5)>(ec);
+    ey[1] = swizzle_d<0x07 | (8 << 5)>(ec);
+    ey[2] = swizzle_d<0x07 | (16 << 5)>(ec);
+    ey[3] = swizzle_d<0x07 | (24 << 5)>(ec);
+  }
+
+  // Pixel part of dphidq for every star of the chain (:365-425 without the
+  // metric / prior terms): lane m receives stars m + 32 t in slot t.
+  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
+                                                  const DT* __restrict__ img, int side,
+                                                  const KRStar* tab, int K,
+                                                  const double (&xs)[SLOTS],
+                                                  const double (&ys)[SLOTS],
+                                                  const bool (&own)[SLOTS], const Consts& c,
+                                                  const LeanConsts& lc, double (&gf)[SLOTS],
+                                                  double (&gx)[SLOTS], double (&gy)[SLOTS]) {
+    const int m = lane_id() & (LPC - 1);
+    const int a = m >> 3, b = m & 7;
+    const int rmax = side - WR, cmax = side - WC;
+    int ro[SLOTS], co[SLOTS];
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      ro[t] = origin(xs[t], WR / 2, rmax);
+      co[t] = origin(ys[t], WC / 2, cmax);
+      gf[t] = gx[t] = gy[t] = 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+#pragma unroll 1
+      for (int kk = 0; kk < LPC; ++kk) {
+        const int k = LPC * t + kk;
+        if (k >= K) break;
+        const KRStar sk = tab[k];
+        const int R0 = origin(sk.x, WR / 2, rmax), C0 = origin(sk.y, WC / 2, cmax);
+        // data pixels of the window (issued before the neighbour work)
+        DT d[NPX];
+        const DT* base = img + (size_t)(R0 + TR * a) * side + (C0 + b);
+#pragma unroll
+        for (int i = 0; i < TR; ++i)
+#pragma unroll
+          for (int j = 0; j < TC; ++j) d[i * TC + j] = base[(size_t)i * side + 8 * j];
+
+        // stars whose windows overlap k's window, union over the two chains
+        unsigned long long nbm = 0ull;
+#pragma unroll
+        for (int t2 = 0; t2 < SLOTS; ++t2) {
+          const int j = LPC * t2 + m;
+          const bool nb = own[t2] && j != k && abs(ro[t2] - R0) < WR && abs(co[t2] - C0) < WC;
+          const unsigned long long bl = __builtin_amdgcn_ballot_w64(nb);
+          nbm |= (unsigned long long)((unsigned)bl | (unsigned)(bl >> 32)) << (LPC * t2);
+        }
+        const double r0 = (double)R0, c0 = (double)C0;
+        double lam[NPX];
+#pragma unroll
+        for (int p = 0; p < NPX; ++p) lam[p] = c.B;
+        while (nbm) {  // wave-uniform
+          const int s = __builtin_ctzll(nbm);
+          nbm &= nbm - 1;
+          const KRStar ss = tab[s];
+          double ex[TR], ey[TC];
+          factors(etab, r0, c0, ss.x, ss.y, a, b, lc, ex, ey);
+#pragma unroll
+          for (int i = 0; i < TR; ++i) {
+            const double fe = ss.f * ex[i];
+#pragma unroll
+            for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(fe, ey[j], lam[i * TC + j]);
+          }
+        }
+        double ex[TR], ey[TC];
+        factors(etab, r0, c0, sk.x, sk.y, a, b, lc, ex, ey);
+#pragma unroll
+        for (int i = 0; i < TR; ++i) {
+          const double fe = sk.f * ex[i];
+#pragma unroll
+          for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(fe, ey[j], lam[i * TC + j]);
+        }
+        // s = D/Lambda - 1, one reciprocal per pixel pair (rhmc_tiledr.hpp)
+        double R[TR], C[TC];
+        auto acc = [&](int pp, double sv) {
+          const int i = pp / TC, j = pp % TC;
+          R[i] = (j == 0) ? ey[j] * sv : fma(ey[j], sv, R[i]);
+          C[j] = (i == 0) ? ex[i] * sv : fma(ex[i], sv, C[j]);
+        };
+#pragma unroll
+        for (int pp = 0; pp < NPX; pp += 2) {
+          const double l0 = lam[pp], l1 = lam[pp + 1];
+          const double L = l0 * l1;
+          const double r = rcp_nr1(L);
+          acc(pp, fma((double)d[pp], l1 * r, -1.0));
+          acc(pp + 1, fma((double)d[pp + 1], l0 * r, -1.0));
+        }
+        double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < TR; ++i) {
+          const double tt = ex[i] * R[i];
+          a0 += tt;
+          a1 = fma(tt, (double)i, a1);
+        }
+#pragma unroll
+        for (int j = 0; j < TC; ++j) {
+          const double w = ey[j] * C[j];
+          w0 += w;
+          w1 = fma(w, (double)(8 * j), w1);
+        }
+        const double dxa = ((r0 + (double)(TR * a)) - sk.x) + 0.5;
+        const double dyb = ((c0 + (double)b) - sk.y) + 0.5;
+        const double s0 = half_sum_dpp(a0);
+        const double s1 = half_sum_dpp(fma(dxa, a0, a1));
+        const double s2 = half_sum_dpp(fma(dyb, w0, w1));
+        if (m == kk) {
+          gf[t] = -s0;                              // :404
+          gx[t] = -s1 * sk.f * lc.inv_var;          // :405
+          gy[t] = -s2 * sk.f * lc.inv_var;          // :406
+        }
+      }
+    }
+    if (c.use_Vc) {  // repulsion (:411-418), O(K^2) from the star table
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        double sx = 0.0, sy = 0.0;
+        for (int jj = 0; jj < K; ++jj) {
+          const KRStar o = tab[jj];
+          const double ddx = o.x - xs[t], ddy = o.y - ys[t];
+          double Rr = sqrt(ddx * ddx + ddy * ddy);
+          if (fabs(Rr) < 1e-10) Rr = 1e32;
+          const double tr = pow(1.0 / Rr, c.vc_pow + 2.0);
+          sx += tr * ddx;
+          sy += tr * ddy;
+        }
+        gx[t] += c.beta * sx * c.vc_pow;
+        gy[t] += c.beta * sy * c.vc_pow;
+      }
+    }
+  }
+};
+
+// The chain's star table: lane m writes its slot stars (f, x, y).
+template <int SLOTS>
+__device__ __forceinline__ void kr_publish(KRStar* tab, const double (&f)[SLOTS],
+                                           const double (&x)[SLOTS], const double (&y)[SLOTS],
+                                           const bool (&own)[SLOTS]) {
+  const int m = lane_id() & 31;
+  wave_lds_sync();  // every lane has finished reading the previous table
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t)
+    if (own[t]) {
+      KRStar e;
+      e.f = f[t];
+      e.x = x[t];
+      e.y = y[t];
+      e.pad = 0.0;
+      tab[32 * t + m] = e;
+    }
+  wave_lds_sync();
+}
+
+// n_steps steps of RHMC_single_step (sampler_RHMC.py:522-566) for the chain's
+// stars (lane m: stars m + 32 t).  The end-of-step gradient is carried into
+// the next step; the flux metric is computed once per distinct f
+// (rhmc_k1step.hpp); the loops stop on np.max(|dq|) <= delta, NaN included.
+template <int SLOTS, class GRAD>
+__device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
+                                         double (&y)[SLOTS], double (&pf)[SLOTS],
+                                         double (&px)[SLOTS], double (&py)[SLOTS],
+                                         const bool (&own)[SLOTS], KRStar* tab, int n_steps,
+                                         double edge, const Consts& c, const LeanConsts& lc,
+                                         GRAD grad, int& it_p, int& it_q, unsigned& st) {
+  const double hdt = c.hdt;
+  FluxMetric fm[SLOTS];
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) fm[t] = flux_metric(f[t], c, lc);
+  kr_publish<SLOTS>(tab, f, x, y, own);
+  for (int s = 0;; ++s) {
+    double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+    grad(x, y, gf, gx, gy);
+    // Recompute the flux metric instead of keeping it live through the
+    // gradient (register pressure): the asm hides f's value from CSE.
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      double fr = f[t];
+      asm volatile("" : "+v"(fr));
+      fm[t] = flux_metric(fr, c, lc);
+    }
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      if (c.use_prior) gf[t] += fm[t].prior;       // :408-409
+      gf[t] += fm[t].mterm;                        // :459-463
+      if (s > 0) {
+        pf[t] = pf[t] - hdt * gf[t];               // :551
+        px[t] = px[t] - hdt * gx[t];
+        py[t] = py[t] - hdt * gy[t];
+        if (f[t] < c.f_lim) {                      // :554-564
+          pf[t] = -pf[t];
+          if (own[t]) st |= RHMC_STATUS_REFLECT_F;
+        }
+        if (x[t] < 0.0 || x[t] > edge) {
+          px[t] = -px[t];
+          if (own[t]) st |= RHMC_STATUS_REFLECT_XY;
+        }
+        if (y[t] < 0.0 || y[t] > edge) {
+          py[t] = -py[t];
+          if (own[t]) st |= RHMC_STATUS_REFLECT_XY;
+        }
+      }
+    }
+    if (s == n_steps) break;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      pf[t] = pf[t] - hdt * gf[t];                 // :525
+      px[t] = px[t] - hdt * gx[t];
+      py[t] = py[t] - hdt * gy[t];
+    }
+    {  // p-loop (:528-535), flux slots only (dtaudq is 0 on x, y)
+      double rho[SLOTS], hc[SLOTS];
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        rho[t] = pf[t];
+        hc[t] = hdt * (fm[t].coef * 0.5);
+      }
+      int n = 0;
+      bool more;
+      do {
+        bool go = false, nan = false;
+#pragma unroll
+        for (int t = 0; t < SLOTS; ++t) {
+          const double P = fma(-hc[t], pf[t] * pf[t], rho[t]);
+          const double d = fabs(pf[t] - P);
+          pf[t] = P;
+          if (own[t]) {
+            go |= d > c.delta;
+            nan |= d != d;
+          }
+        }
+        ++n;
+        more = half_any(go) && !half_any(nan);
+      } while (more && n < c.counter_max);
+      it_p += n;
+      if (more) st |= RHMC_STATUS_PLOOP_CAP;
+    }
+    {  // q-loop (:538-545): q' = q_s + hdt (p/H(q_s) + p/H(q)), affine in f and g(f)
+      double bf[SLOTS], cf[SLOTS], bx[SLOTS], cx[SLOTS], by[SLOTS], cy[SLOTS];
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const double ihxx_s = fm[t].s * lc.inv_gxx;
+        bf[t] = hdt * (pf[t] * lc.inv_gff2);
+        cf[t] = f[t] + hdt * (pf[t] * fm[t].A + pf[t] * lc.c0);
+        bx[t] = hdt * (px[t] * lc.inv_gxx);
+        cx[t] = x[t] + hdt * (px[t] * ihxx_s);
+        by[t] = hdt * (py[t] * lc.inv_gxx);
+        cy[t] = y[t] + hdt * (py[t] * ihxx_s);
+      }
+      int n = 0;
+      bool more;
+      do {
+        bool go = false, nan = false;
+#pragma unroll
+        for (int t = 0; t < SLOTS; ++t) {
+          const double F = fma(bf[t], f[t], cf[t]);
+          const double fl = (f[t] < lc.f_low) ? lc.f_low : f[t];
+          const double u = rcp_nr1(fl);
+          const double g = u * fma(lc.Bg2, u, lc.inv_g1);
+          const double X = fma(bx[t], g, cx[t]);
+          const double Y = fma(by[t], g, cy[t]);
+          const double a0 = fabs(f[t] - F), a1 = fabs(x[t] - X), a2 = fabs(y[t] - Y);
+          const double sum = a0 + a1 + a2;
+          f[t] = F;
+          x[t] = X;
+          y[t] = Y;
+          if (own[t]) {
+            go |= fmax(fmax(a0, a1), a2) > c.delta;
+            nan |= sum != sum;
+          }
+        }
+        ++n;
+        more = half_any(go) && !half_any(nan);
+      } while (more && n < c.counter_max);
+      it_q += n;
+      if (more) st |= RHMC_STATUS_QLOOP_CAP;
+    }
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      fm[t] = flux_metric(f[t], c, lc);
+      pf[t] = pf[t] - hdt * ((pf[t] * pf[t]) * fm[t].coef / 2.0);  // :548
+    }
+    kr_publish<SLOTS>(tab, f, x, y, own);
+  }
+}
+
+// Two chains per wave (32 lanes each), W waves per workgroup; two waves per
+// SIMD (<= 256 VGPRs) except the fp64-image / K > 32 variant, which needs more.
+template <typename DT, int SLOTS>
+__global__ void __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(sizeof(DT) == 8 && SLOTS == 2 ? 1 : 2)))
+leapfrog_kr(LeapArgsKR a) {
+  using TK = TiledRK<DT, SLOTS>;
+  extern __shared__ double lds[];
+  const DT* img;
+  if constexpr (sizeof(DT) == sizeof(float)) img = reinterpret_cast<const DT*>(a.Df);
+  else img = reinterpret_cast<const DT*>(a.D);
+  exp_tab_fill(lds);
+  __syncthreads();
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  if (TK::CPW * wave >= a.n_chains) return;
+  const int lane = lane_id();
+  const int h = lane / TK::LPC, m = lane % TK::LPC;
+  const int64_t chain = TK::CPW * wave + h;
+  const bool real = chain < a.n_chains;  // ragged tail: mirror the wave's first chain
+  const int64_t cbase = (real ? chain : TK::CPW * wave) * 3 * (int64_t)a.K;
+  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) +
+                ((threadIdx.x / kWave) * TK::CPW + h) * TK::KMAX;
+  const Consts& c = a.c;
+  const LeanConsts lc = lean_consts(c);
+  const int K = a.K;
+
+  double f[SLOTS], x[SLOTS], y[SLOTS], pf[SLOTS], px[SLOTS], py[SLOTS];
+  bool own[SLOTS];
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    const int j = TK::LPC * t + m;
+    own[t] = j < K;
+    const int64_t e = cbase + 3 * (int64_t)(own[t] ? j : 0);
+    f[t] = own[t] ? a.q[e] : 1.0;
+    x[t] = own[t] ? a.q[e + 1] : 0.0;
+    y[t] = own[t] ? a.q[e + 2] : 0.0;
+    pf[t] = own[t] ? a.p[e] : 0.0;
+    px[t] = own[t] ? a.p[e + 1] : 0.0;
+    py[t] = own[t] ? a.p[e + 2] : 0.0;
+  }
+  int it_p = 0, it_q = 0;
+  unsigned st = 0u;
+  const int side = a.side;
+  km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc,
+                  [&](const double (&xs)[SLOTS], const double (&ys)[SLOTS], double (&gf)[SLOTS],
+                      double (&gx)[SLOTS], double (&gy)[SLOTS]) {
+                    TK::gradient(lds, img, side, tab, K, xs, ys, own, c, lc, gf, gx, gy);
+                  },
+                  it_p, it_q, st);
+
+  unsigned nf = 0u;
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    if (!own[t] || !real) continue;
+    if (!(isfinite(f[t]) && isfinite(x[t]) && isfinite(y[t]) && isfinite(pf[t]) &&
+          isfinite(px[t]) && isfinite(py[t])))
+      nf = RHMC_STATUS_NONFINITE;
+    const int64_t e = cbase + 3 * (int64_t)(TK::LPC * t + m);
+    a.q[e] = f[t];
+    a.q[e + 1] = x[t];
+    a.q[e + 2] = y[t];
+    a.p[e] = pf[t];
+    a.p[e + 1] = px[t];
+    a.p[e + 2] = py[t];
+  }
+  unsigned all = st | nf;
+#pragma unroll
+  for (int d = 16; d >= 1; d >>= 1) all |= (unsigned)__shfl_xor((int)all, d, kWave);
+  if (m == 0 && real) {
+    if (a.status) a.status[chain] = (int32_t)all;
+    if (a.fp_iters) {
+      a.fp_iters[2 * chain] = it_p;
+      a.fp_iters[2 * chain + 1] = it_q;
+    }
+  }
+}
+
+}  // namespace rhmc
