@@ -1122,38 +1122,49 @@ bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c) {
          reg_window_ok(28, c.inv_two_sig2);
 }
 
-// Which multi-star kernel serves (K, image) by default: the full-image tiled
-// kernel (rhmc_tiledk.hpp) on 32x32 / 48x48 images with K <= 16, where every
-// star's window covers most of the image (C3: 20.1 vs 22.5 ms per 100 steps),
-// the register-window kernel elsewhere (C5: 3.2x the windowed kernel).
-// RHMC_KERNEL=tiledrk / tiledk / windowed / generic force a family.
+// Which multi-star kernel serves (K, image) by default: the register-window
+// kernel wherever it applies (C3 with LDS factor tables: 18.0 ms per 100 steps
+// against 20.3 for the full-image tiled kernel; C5: 3.2x the windowed kernel).
+// RHMC_KERNEL=tiledk / windowed / generic force the older families.
 bool use_tiledrk(const rhmc_ctx* ctx, int K, const Consts& c) {
   const char* e = std::getenv("RHMC_KERNEL");
   if (e && (std::strcmp(e, "tiledk") == 0 || std::strcmp(e, "windowed") == 0 ||
             std::strcmp(e, "generic") == 0))
     return false;
-  if (!tiledrk_ok(ctx, K, c)) return false;
-  if (e && std::strcmp(e, "tiledrk") == 0) return true;
-  return !((ctx->rows == 32 || ctx->rows == 48) && K <= kMaxKGeneric);
+  return tiledrk_ok(ctx, K, c);
 }
 
-template <typename DT, int SLOTS>
+template <typename DT, int SLOTS, bool TAB>
 int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, hipStream_t s) {
-  using TK = TiledRK<DT, SLOTS>;
-  constexpr int W = 4;
-  const size_t lds = TK::lds_bytes(W);
+  using TK = TiledRK<DT, SLOTS, TAB>;
+  int W = 4;
+  while (W > 1 && TK::lds_bytes(W, a.K, a.side) > (size_t)ctx->max_lds / 2) W >>= 1;
+  const size_t lds = TK::lds_bytes(W, a.K, a.side);
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "factor tables exceed LDS");
   const int64_t waves = (a.n_chains + TK::CPW - 1) / TK::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS, TAB>), grid, block, lds, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
+}
+
+// Factor tables in LDS (TiledRK<..., TAB>) for images up to 64 px with K <= 16,
+// where every window overlaps (nearly) every star; RHMC_KERNEL=tiledrk_notab
+// forces the exp path there.
+bool kr_tables(const rhmc_ctx* ctx, int K) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  if (e && std::strcmp(e, "tiledrk_notab") == 0) return false;
+  return ctx->rows <= 64 && K <= 16;
 }
 
 int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
   const bool f32 = ctx->img_f32;
   if (f32) a.Df = ctx->d_Df;
-  if (a.K <= 32) return f32 ? launch_kr_t<float, 1>(ctx, a, s) : launch_kr_t<double, 1>(ctx, a, s);
-  return f32 ? launch_kr_t<float, 2>(ctx, a, s) : launch_kr_t<double, 2>(ctx, a, s);
+  if (kr_tables(ctx, a.K))
+    return f32 ? launch_kr_t<float, 1, true>(ctx, a, s) : launch_kr_t<double, 1, true>(ctx, a, s);
+  if (a.K <= 32)
+    return f32 ? launch_kr_t<float, 1, false>(ctx, a, s) : launch_kr_t<double, 1, false>(ctx, a, s);
+  return f32 ? launch_kr_t<float, 2, false>(ctx, a, s) : launch_kr_t<double, 2, false>(ctx, a, s);
 }
 
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,

@@ -63,7 +63,11 @@ __device__ __forceinline__ bool half_any(bool v) {
   return (lane_id() < 32 ? lo : hi) != 0u;
 }
 
-template <typename DT, int SLOTS>
+// TAB: PSF factors read from per-chain LDS tables over the whole image
+// (K x (rows + cols) doubles, rebuilt once per gradient) instead of two exps
+// and eleven swizzles per (window, star) pair — for small images, where every
+// window overlaps every other star's (C3: 48x48, K = 10).
+template <typename DT, int SLOTS, bool TAB = false>
 struct TiledRK {
   static constexpr int LPC = 32;           // lanes per chain
   static constexpr int CPW = kWave / LPC;  // chains per wave
@@ -73,8 +77,9 @@ struct TiledRK {
   static constexpr int NPX = TR * TC;
   static_assert(SLOTS == 1 || SLOTS == 2, "K <= 64");
 
-  static __host__ __device__ constexpr size_t lds_bytes(int waves) {
-    return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar);
+  static __host__ __device__ constexpr size_t lds_bytes(int waves, int K, int side) {
+    return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar) +
+           (TAB ? (size_t)waves * CPW * K * 2 * side * sizeof(double) : 0);
   }
   static __device__ __forceinline__ int origin(double v, int half, int omax) {
     if (!(fabs(v) < 1.0e7)) return 0;
@@ -106,11 +111,48 @@ struct TiledRK {
     ey[3] = swizzle_d<0x07 | (24 << 5)>(ec);
   }
 
+  // TAB: the chain's factor tables, [K][rows | cols] (utils.py:475-486 per axis).
+  static __device__ __forceinline__ void build_tables(const double* __restrict__ etab,
+                                                      double* ftab, const KRStar* tab, int K,
+                                                      int side, const LeanConsts& lc) {
+    const int m = lane_id() & (LPC - 1);
+    const int per = 2 * side, total = K * per;
+    wave_lds_sync();  // the previous gradient's reads are done
+    for (int e = m; e < total; e += LPC) {
+      const int k = e / per, r = e - k * per;
+      const bool col = r >= side;
+      const int i = col ? r - side : r;
+      const KRStar sk = tab[k];
+      const double v = ((double)i + 0.5) - (col ? sk.y : sk.x);
+      const double val = exp_neg(-(v * v) * lc.inv_two_sig2, etab);
+      ftab[e] = col ? val * lc.inv_norm : val;
+    }
+    wave_lds_sync();
+  }
+
+  // Factors of star s on the window (R0, C0): exps + swizzles, or table reads.
+  static __device__ __forceinline__ void star_factors(const double* __restrict__ etab,
+                                                      const double* ftab, int side, int s,
+                                                      const KRStar& ss, int R0, int C0, int a,
+                                                      int b, const LeanConsts& lc,
+                                                      double (&ex)[TR], double (&ey)[TC]) {
+    if constexpr (TAB) {
+      const double* tr = ftab + (size_t)s * 2 * side + R0 + TR * a;
+      const double* tc = ftab + (size_t)s * 2 * side + side + C0 + b;
+#pragma unroll
+      for (int i = 0; i < TR; ++i) ex[i] = tr[i];
+#pragma unroll
+      for (int j = 0; j < TC; ++j) ey[j] = tc[8 * j];
+    } else {
+      factors(etab, (double)R0, (double)C0, ss.x, ss.y, a, b, lc, ex, ey);
+    }
+  }
+
   // Pixel part of dphidq for every star of the chain (:365-425 without the
   // metric / prior terms): lane m receives stars m + 32 t in slot t.
   static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
                                                   const DT* __restrict__ img, int side,
-                                                  const KRStar* tab, int K,
+                                                  const KRStar* tab, double* ftab, int K,
                                                   const double (&xs)[SLOTS],
                                                   const double (&ys)[SLOTS],
                                                   const bool (&own)[SLOTS], const Consts& c,
@@ -119,6 +161,7 @@ struct TiledRK {
     const int m = lane_id() & (LPC - 1);
     const int a = m >> 3, b = m & 7;
     const int rmax = side - WR, cmax = side - WC;
+    if constexpr (TAB) build_tables(etab, ftab, tab, K, side, lc);
     int ro[SLOTS], co[SLOTS];
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) {
@@ -160,7 +203,7 @@ struct TiledRK {
           nbm &= nbm - 1;
           const KRStar ss = tab[s];
           double ex[TR], ey[TC];
-          factors(etab, r0, c0, ss.x, ss.y, a, b, lc, ex, ey);
+          star_factors(etab, ftab, side, s, ss, R0, C0, a, b, lc, ex, ey);
 #pragma unroll
           for (int i = 0; i < TR; ++i) {
             const double fe = ss.f * ex[i];
@@ -169,7 +212,7 @@ struct TiledRK {
           }
         }
         double ex[TR], ey[TC];
-        factors(etab, r0, c0, sk.x, sk.y, a, b, lc, ex, ey);
+        star_factors(etab, ftab, side, k, sk, R0, C0, a, b, lc, ex, ey);
 #pragma unroll
         for (int i = 0; i < TR; ++i) {
           const double fe = sk.f * ex[i];
@@ -390,11 +433,11 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
 
 // Two chains per wave (32 lanes each), W waves per workgroup; two waves per
 // SIMD (<= 256 VGPRs) except the fp64-image / K > 32 variant, which needs more.
-template <typename DT, int SLOTS>
+template <typename DT, int SLOTS, bool TAB>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(sizeof(DT) == 8 && SLOTS == 2 ? 1 : 2)))
 leapfrog_kr(LeapArgsKR a) {
-  using TK = TiledRK<DT, SLOTS>;
+  using TK = TiledRK<DT, SLOTS, TAB>;
   extern __shared__ double lds[];
   const DT* img;
   if constexpr (sizeof(DT) == sizeof(float)) img = reinterpret_cast<const DT*>(a.Df);
@@ -408,8 +451,11 @@ leapfrog_kr(LeapArgsKR a) {
   const int64_t chain = TK::CPW * wave + h;
   const bool real = chain < a.n_chains;  // ragged tail: mirror the wave's first chain
   const int64_t cbase = (real ? chain : TK::CPW * wave) * 3 * (int64_t)a.K;
-  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) +
-                ((threadIdx.x / kWave) * TK::CPW + h) * TK::KMAX;
+  const int W = blockDim.x / kWave;
+  const int slot = (threadIdx.x / kWave) * TK::CPW + h;  // chain slot in the workgroup
+  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * TK::KMAX;
+  double* ftab = lds + kExpTab + (size_t)W * TK::CPW * TK::KMAX * (sizeof(KRStar) / 8) +
+                 (size_t)slot * a.K * 2 * a.side;  // TAB only
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
   const int K = a.K;
@@ -434,7 +480,7 @@ leapfrog_kr(LeapArgsKR a) {
   km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc,
                   [&](const double (&xs)[SLOTS], const double (&ys)[SLOTS], double (&gf)[SLOTS],
                       double (&gx)[SLOTS], double (&gy)[SLOTS]) {
-                    TK::gradient(lds, img, side, tab, K, xs, ys, own, c, lc, gf, gx, gy);
+                    TK::gradient(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy);
                   },
                   it_p, it_q, st);
 
