@@ -284,8 +284,13 @@ def main():
     traffic = pmc.get("hbm_bytes_per_launch")
     if traffic is not None and pmc.get("chain_steps_per_dispatch") not in (None, chain_steps):
         traffic = traffic * chain_steps / pmc["chain_steps_per_dispatch"]
+    metric = "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X"
+    if wl.name != "C2" or args.chains or args.global_chains or args.mode != "leapfrog":
+        # not the headline configuration: name what was run
+        metric = "chain-leapfrog-steps/sec, %s %dx%d %d-star %d chains/GPU (%s)" % (
+            wl.name, wl.D.shape[0], wl.D.shape[1], wl.K, wl.n_chains, args.mode)
     out = {
-        "metric": "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X",
+        "metric": metric,
         "value": value,
         "unit": "chain-leapfrog-steps/s",
         "n_gpus": world,

@@ -1118,7 +1118,7 @@ int dispatch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
 // Multi-star register-window kernel (rhmc_tiledrk.hpp): K in [2, 64], square
 // image of side >= 32, PSF narrow enough for the 28-row window.
 bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c) {
-  return K >= 2 && K <= 64 && ctx->rows == ctx->cols && ctx->rows >= 32 &&
+  return K >= 1 && K <= 64 && ctx->rows == ctx->cols && ctx->rows >= 32 &&
          reg_window_ok(28, c.inv_two_sig2);
 }
 
@@ -1178,8 +1178,10 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   if (n_chains == 0) return RHMC_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const int side = ctx->rows;
+  const char* kenv = std::getenv("RHMC_KERNEL");
+  const bool kr_k1 = K == 1 && kenv && std::strncmp(kenv, "tiledrk", 7) == 0;  // experiment
   const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
-                  !force_windowed();
+                  !force_windowed() && !kr_k1;
   const char* ke = std::getenv("RHMC_KERNEL");
   const bool img_ok = side == 32 || side == 48 || side == 64 || side == 96 || side == 128;
   // register-window kernel (default) / LDS-operand window kernel (tiledw*)
