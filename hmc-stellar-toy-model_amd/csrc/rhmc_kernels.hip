@@ -32,6 +32,7 @@
 #include "rhmc_tiled.hpp"
 #include "rhmc_tiled2.hpp"
 #include "rhmc_tiledk.hpp"
+#include "rhmc_tiledl.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
 #include "rhmc_tiledw.hpp"
@@ -818,7 +819,7 @@ int window_unsupported() {
 bool force_full_image_k1() {
   const char* e = std::getenv("RHMC_KERNEL");
   return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiledr", 6) != 0 &&
-         std::strncmp(e, "tiled", 5) == 0;
+         std::strncmp(e, "tiledl", 6) != 0 && std::strncmp(e, "tiled", 5) == 0;
 }
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
@@ -1050,6 +1051,49 @@ int launch_tiledr(const rhmc_ctx* ctx, LeapArgsK1 a, hipStream_t s) {
              : launch_tiledr_t<IMG, 32, double, false>(ctx, a, s);
 }
 
+// Lane-group single-star kernel for large batches (rhmc_tiledl.hpp).
+template <int IMG, typename DT, int LPC>
+int launch_tiledl_t(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
+  using TL = TiledL<IMG, 28, DT, LPC>;
+  const size_t lds = TL::lds_bytes();
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+  constexpr int W = 4;
+  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_k1_tiledl<IMG, 28, DT, LPC>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+template <int IMG, int LPC>
+int launch_tiledl_lpc(const rhmc_ctx* ctx, LeapArgsK1 a, bool f32, hipStream_t s) {
+  if (f32) {
+    a.Df = ctx->d_Df;
+    return launch_tiledl_t<IMG, float, LPC>(ctx, a, s);
+  }
+  return launch_tiledl_t<IMG, double, LPC>(ctx, a, s);
+}
+
+// Lanes per chain of the lane-group kernel for a K = 1 batch of n chains, or 0
+// for the register-window kernel.  RHMC_KERNEL=tiledl1 / tiledl4 force it
+// (suffix _64: fp64 image in LDS); any other forced kernel turns it off.
+// Measured (C2 geometry, 500 steps, chain-steps/s): 16384 chains tiledr
+// 1.99e9 / LPC 4 2.25e9; 65536: 2.28e9 / LPC 1 3.06e9; 131072: 2.31e9 / 3.59e9.
+constexpr int64_t kLaneChains1 = 65536;   // >= one 64-chain wave per SIMD
+constexpr int64_t kLaneChains4 = 16384;   // >= one 16-chain wave per SIMD
+int tiledl_lpc(int64_t n, const char* e) {
+  if (e && std::strncmp(e, "tiledl", 6) == 0) return e[6] == '4' ? 4 : 1;
+  if (e) return 0;
+  return n >= kLaneChains1 ? 1 : n >= kLaneChains4 ? 4 : 0;
+}
+
+template <int IMG>
+int launch_tiledl(const rhmc_ctx* ctx, const LeapArgsK1& a, int lpc, hipStream_t s) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  const bool f32 = ctx->img_f32 && !(e && std::strstr(e, "_64"));
+  return lpc == 4 ? launch_tiledl_lpc<IMG, 4>(ctx, a, f32, s)
+                  : launch_tiledl_lpc<IMG, 1>(ctx, a, f32, s);
+}
+
 // Windowed single-star kernels: register-window (default, RHMC_KERNEL=tiledr)
 // or the LDS-operand kernel with 16 / 32 lanes per chain (tiledw / tiledw32).
 template <int IMG>
@@ -1205,6 +1249,14 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.Df = nullptr;
     t.c = a.c;
     if (k1r) {
+      const int lpc = tiledl_lpc(n_chains, ke);
+      if (lpc && side <= 64 && reg_window_ok(28, a.c.inv_two_sig2)) {
+        switch (side) {
+          case 32: return launch_tiledl<32>(ctx, t, lpc, s);
+          case 48: return launch_tiledl<48>(ctx, t, lpc, s);
+          default: return launch_tiledl<64>(ctx, t, lpc, s);
+        }
+      }
       switch (side) {
         case 32: return launch_tiledr<32>(ctx, t, s);
         case 48: return launch_tiledr<48>(ctx, t, s);
