@@ -778,6 +778,7 @@ struct rhmc_ctx {
   void* mh_scratch = nullptr;      // MH driver work arrays (q', p, V, V', E0)
   size_t mh_scratch_bytes = 0;
   int max_lds = 0;
+  int n_cu = 0;
 };
 
 namespace {
@@ -1021,11 +1022,18 @@ int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
 template <int IMG, int WIN, typename DT, bool PROF>
 int launch_tiledr_t(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   using TL = TiledR<IMG, WIN, DT>;
-  const size_t lds = TL::lds_bytes();
+  size_t lds = TL::lds_bytes();
   if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
   constexpr int W = 4;
   const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  // RHMC_LDS_MIN pads the LDS request (experiment: 82 KB = one workgroup per
+  // CU; at C2 the dispatcher already spreads the 256 workgroups one per CU:
+  // 1.2255 vs 1.2251 ms per launch, measured).
+  if (const char* pad = std::getenv("RHMC_LDS_MIN")) {
+    const size_t want = (size_t)std::atol(pad);
+    if (want <= (size_t)ctx->max_lds && want >= TL::lds_bytes()) lds = want;
+  }
   hipLaunchKernelGGL((leapfrog_k1_tiledr<IMG, WIN, DT, PROF>), grid, block, lds, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
@@ -1584,6 +1592,7 @@ int rhmc_ctx_create(int device, const double* D, int32_t rows, int32_t cols, rhm
     return fail(RHMC_ERR_HIP, "hipGetDeviceProperties failed");
   }
   ctx->max_lds = (int)prop.sharedMemPerBlock;
+  ctx->n_cu = prop.multiProcessorCount;
   if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     delete ctx;
     return fail(RHMC_ERR_HIP, "hipStreamCreate failed");
