@@ -187,6 +187,9 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     from rhmc_amd import shard, workloads
+    if args.workload.upper() == "C4" and not args.chains and not args.global_chains:
+        # C4 is one 2^20-chain set sharded over the ranks (BASELINE configs[3])
+        args.global_chains = 1 << 20
     if args.global_chains:
         # one global chain set (seed 1000), this rank's contiguous shard
         wl = workloads.make(args.workload, n_chains=args.global_chains)
