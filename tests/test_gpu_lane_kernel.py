@@ -1,0 +1,103 @@
+"""The lane-group single-star kernel (rhmc_tiledl.hpp) at the batch sizes
+where launch_leapfrog switches to it, through the C-ABI.
+
+* threshold and ragged batches (16383 / 16384 / 65537 chains): every chain
+  agrees with the register-window kernel run on the same states to 1e-10
+  (q) / 1e-9 (p) relative to |value| + 1 after 50 steps, with identical
+  fixed-point iteration counts on all but a handful of chains (a count can
+  only differ where an iterate lands within rounding of delta), and a
+  seeded sample matches the CPU oracle (SURVEY §8(c) tolerance);
+* 64x64 and 32x32 images (the other LDS layouts) against the oracle;
+* a non-finite chain stays confined to itself and is flagged.
+"""
+import numpy as np
+import pytest
+
+from helpers import assert_state_close
+from oracle import rhmc_ref as R
+from rhmc_amd import workloads
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 50
+
+
+def _par(wl):
+    par = dict(wl.params)
+    par["rows"], par["cols"] = wl.D.shape
+    return par
+
+
+def _run(capi, ctx, P, q0, p0, kernel, monkeypatch, steps=STEPS):
+    if kernel:
+        monkeypatch.setenv("RHMC_KERNEL", kernel)
+    else:
+        monkeypatch.delenv("RHMC_KERNEL", raising=False)
+    return ctx.leapfrog(P, q0, p0, steps, return_info=True)
+
+
+@pytest.mark.parametrize("n", [16383, 16384, 65537])
+def test_threshold_batches_match_register_window_and_oracle(gpu_lib, monkeypatch, n):
+    capi = gpu_lib
+    wl = workloads.make("C2", n_chains=n)
+    ctx = capi.Context(wl.D)
+    P = capi.make_params(**wl.params)
+    q, p, it, st = _run(capi, ctx, P, wl.q0, wl.p0, None, monkeypatch)       # default choice
+    qr, pr, itr, str_ = _run(capi, ctx, P, wl.q0, wl.p0, "tiledr", monkeypatch)
+    assert not (st & capi.STATUS_NONFINITE).any()
+    eq = np.abs(q - qr) / (np.abs(qr) + 1)
+    ep = np.abs(p - pr) / (np.abs(pr) + 1)
+    assert eq.max() <= 1e-10 and ep.max() <= 1e-9, (eq.max(), ep.max())
+    assert (it != itr).any(axis=1).sum() <= max(2, n // 5000)
+    m = R.RefModel(wl.D, _par(wl))
+    for c in (0, n // 2, n - 1):
+        qo, po, NP, NQ = m.trajectory(wl.q0[c], wl.p0[c], STEPS, record=False)
+        assert it[c, 0] == NP.sum() and it[c, 1] == NQ.sum(), c
+        assert_state_close(q[c], qo, 1e-9, "q chain %d" % c)
+        assert_state_close(p[c], po, 1e-8, "p chain %d" % c)
+    ctx.close()
+
+
+@pytest.mark.parametrize("side", [32, 64])
+@pytest.mark.parametrize("kernel", ["tiledl1", "tiledl4"])
+def test_other_image_sides_vs_oracle(gpu_lib, monkeypatch, side, kernel):
+    capi = gpu_lib
+    wl = workloads.make("C2", n_chains=6)
+    rs = np.random.RandomState(side)
+    D = rs.poisson(wl.params["B_count"], size=(side, side)).astype(np.float64)
+    c = side / 2.0
+    D[int(c) - 2:int(c) + 2, int(c) - 2:int(c) + 2] += 60.0   # a faint source near the centre
+    q0 = wl.q0.copy()
+    q0[:, 1] += c - 24.0
+    q0[:, 2] += c - 24.0
+    q0[0, 1] = 1.2                                          # clamped windows, near an edge
+    q0[1, 2] = side - 1.7
+    ctx = capi.Context(D)
+    P = capi.make_params(**wl.params)
+    q, p, it, st = _run(capi, ctx, P, q0, wl.p0, kernel, monkeypatch, steps=40)
+    par = dict(wl.params)
+    par["rows"] = par["cols"] = side
+    m = R.RefModel(D, par)
+    for k in range(len(q0)):
+        qo, po, NP, NQ = m.trajectory(q0[k], wl.p0[k], 40, record=False)
+        assert it[k, 0] == NP.sum() and it[k, 1] == NQ.sum(), k
+        assert_state_close(q[k], qo, 1e-9, "q chain %d" % k)
+        assert_state_close(p[k], po, 1e-8, "p chain %d" % k)
+    ctx.close()
+
+
+@pytest.mark.parametrize("kernel", ["tiledl1", "tiledl4"])
+def test_nonfinite_chain_is_confined(gpu_lib, monkeypatch, kernel):
+    capi = gpu_lib
+    wl = workloads.make("C2", n_chains=70)
+    q0 = wl.q0.copy()
+    q0[5, 1] = np.nan
+    ctx = capi.Context(wl.D)
+    P = capi.make_params(**wl.params)
+    q, p, it, st = _run(capi, ctx, P, q0, wl.p0, kernel, monkeypatch, steps=10)
+    bad = (st & capi.STATUS_NONFINITE) != 0
+    assert bad[5] and bad.sum() == 1
+    qc, pc, _, _ = _run(capi, ctx, P, np.delete(q0, 5, 0), np.delete(wl.p0, 5, 0), kernel,
+                        monkeypatch, steps=10)
+    assert np.array_equal(np.delete(q, 5, 0), qc) and np.array_equal(np.delete(p, 5, 0), pc)
+    ctx.close()
