@@ -56,6 +56,14 @@ struct KRStar {  // LDS star table entry
   double f, x, y, pad;
 };
 
+// TAB variant: Lambda over all stars in an unrolled loop (A/B knob), for at
+// most TABK stars (kr_tables in rhmc_kernels.hip: K <= 16).
+#ifndef RHMC_KR_ALLSTARS
+#define RHMC_KR_ALLSTARS 1
+#endif
+constexpr bool kAllStarsTab = RHMC_KR_ALLSTARS;
+constexpr int TABK = 16;
+
 // This chain's half of a wave ballot (lanes 0-31 or 32-63).
 __device__ __forceinline__ bool half_any(bool v) {
   const unsigned long long b = __builtin_amdgcn_ballot_w64(v);
@@ -185,40 +193,56 @@ struct TiledRK {
 #pragma unroll
           for (int j = 0; j < TC; ++j) d[i * TC + j] = base[(size_t)i * side + 8 * j];
 
-        // stars whose windows overlap k's window, union over the two chains
-        unsigned long long nbm = 0ull;
-#pragma unroll
-        for (int t2 = 0; t2 < SLOTS; ++t2) {
-          const int j = LPC * t2 + m;
-          const bool nb = own[t2] && j != k && abs(ro[t2] - R0) < WR && abs(co[t2] - C0) < WC;
-          const unsigned long long bl = __builtin_amdgcn_ballot_w64(nb);
-          nbm |= (unsigned long long)((unsigned)bl | (unsigned)(bl >> 32)) << (LPC * t2);
-        }
         const double r0 = (double)R0, c0 = (double)C0;
         double lam[NPX];
 #pragma unroll
         for (int p = 0; p < NPX; ++p) lam[p] = c.B;
-        while (nbm) {  // wave-uniform
-          const int s = __builtin_ctzll(nbm);
-          nbm &= nbm - 1;
-          const KRStar ss = tab[s];
-          double ex[TR], ey[TC];
-          star_factors(etab, ftab, side, s, ss, R0, C0, a, b, lc, ex, ey);
+        auto add_star = [&](double fs, const double (&ex)[TR], const double (&ey)[TC]) {
+          // f scales the TC column factors (fewer products than the TR rows)
+          double fy[TC];
 #pragma unroll
-          for (int i = 0; i < TR; ++i) {
-            const double fe = ss.f * ex[i];
+          for (int j = 0; j < TC; ++j) fy[j] = fs * ey[j];
 #pragma unroll
-            for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(fe, ey[j], lam[i * TC + j]);
+          for (int i = 0; i < TR; ++i)
+#pragma unroll
+            for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], lam[i * TC + j]);
+        };
+        if constexpr (TAB && kAllStarsTab) {
+          // Small images (C3): nearly every window overlaps every star, so
+          // Lambda sums ALL the chain's stars in ascending order, as the
+          // reference does (:373-376), in a fully unrolled loop: table reads
+          // at constant offsets and no mask bookkeeping.  A star whose window
+          // misses k's adds less than half an ulp of B (the window bound).
+#pragma unroll
+          for (int s = 0; s < TABK; ++s) {
+            if (s < K) {  // wave-uniform
+              double ex[TR], ey[TC];
+              star_factors(etab, ftab, side, s, tab[s], R0, C0, a, b, lc, ex, ey);
+              add_star(tab[s].f, ex, ey);
+            }
+          }
+        } else {
+          // stars whose windows overlap k's window, union over the two chains
+          unsigned long long nbm = 0ull;
+#pragma unroll
+          for (int t2 = 0; t2 < SLOTS; ++t2) {
+            const int j = LPC * t2 + m;
+            const bool nb = own[t2] && j != k && abs(ro[t2] - R0) < WR && abs(co[t2] - C0) < WC;
+            const unsigned long long bl = __builtin_amdgcn_ballot_w64(nb);
+            nbm |= (unsigned long long)((unsigned)bl | (unsigned)(bl >> 32)) << (LPC * t2);
+          }
+          while (nbm) {  // wave-uniform
+            const int s = __builtin_ctzll(nbm);
+            nbm &= nbm - 1;
+            const KRStar ss = tab[s];
+            double ex[TR], ey[TC];
+            star_factors(etab, ftab, side, s, ss, R0, C0, a, b, lc, ex, ey);
+            add_star(ss.f, ex, ey);
           }
         }
         double ex[TR], ey[TC];
         star_factors(etab, ftab, side, k, sk, R0, C0, a, b, lc, ex, ey);
-#pragma unroll
-        for (int i = 0; i < TR; ++i) {
-          const double fe = sk.f * ex[i];
-#pragma unroll
-          for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(fe, ey[j], lam[i * TC + j]);
-        }
+        if constexpr (!(TAB && kAllStarsTab)) add_star(sk.f, ex, ey);
         // s = D/Lambda - 1, one reciprocal per pixel pair (rhmc_tiledr.hpp)
         double R[TR], C[TC];
         auto acc = [&](int pp, double sv) {
