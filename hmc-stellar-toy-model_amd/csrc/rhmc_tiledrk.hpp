@@ -63,6 +63,11 @@ struct KRStar {  // LDS star table entry
 #endif
 constexpr bool kAllStarsTab = RHMC_KR_ALLSTARS;
 constexpr int TABK = 16;
+// TAB variant: the image staged in LDS instead of read from L2 (A/B knob).
+#ifndef RHMC_KR_IMG_LDS
+#define RHMC_KR_IMG_LDS 1
+#endif
+constexpr bool kImgLds = RHMC_KR_IMG_LDS;
 
 // This chain's half of a wave ballot (lanes 0-31 or 32-63).
 __device__ __forceinline__ bool half_any(bool v) {
@@ -84,10 +89,17 @@ struct TiledRK {
   static constexpr int TR = 7, TC = 4;     // rows x columns per lane
   static constexpr int NPX = TR * TC;
   static_assert(SLOTS == 1 || SLOTS == 2, "K <= 64");
+  // all-stars Lambda loop: fp32-image variant only (the fp64-image one would
+  // spill: its window pixels take twice the registers)
+  static constexpr bool kAll = TAB && kAllStarsTab && sizeof(DT) == sizeof(float);
 
+  // LDS: exp table, per-chain star tables, then (TAB) per-chain factor tables
+  // and the image (DT [side][side], read by every window of the workgroup).
   static __host__ __device__ constexpr size_t lds_bytes(int waves, int K, int side) {
     return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar) +
-           (TAB ? (size_t)waves * CPW * K * 2 * side * sizeof(double) : 0);
+           (TAB ? (size_t)waves * CPW * K * 2 * side * sizeof(double) +
+                      (kImgLds ? (size_t)side * side * sizeof(DT) : 0)
+                : 0);
   }
   static __device__ __forceinline__ int origin(double v, int half, int omax) {
     if (!(fabs(v) < 1.0e7)) return 0;
@@ -207,7 +219,7 @@ struct TiledRK {
 #pragma unroll
             for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], lam[i * TC + j]);
         };
-        if constexpr (TAB && kAllStarsTab) {
+        if constexpr (kAll) {
           // Small images (C3): nearly every window overlaps every star, so
           // Lambda sums ALL the chain's stars in ascending order, as the
           // reference does (:373-376), in a fully unrolled loop: table reads
@@ -242,7 +254,7 @@ struct TiledRK {
         }
         double ex[TR], ey[TC];
         star_factors(etab, ftab, side, k, sk, R0, C0, a, b, lc, ex, ey);
-        if constexpr (!(TAB && kAllStarsTab)) add_star(sk.f, ex, ey);
+        if constexpr (!kAll) add_star(sk.f, ex, ey);
         // s = D/Lambda - 1, one reciprocal per pixel pair (rhmc_tiledr.hpp)
         double R[TR], C[TC];
         auto acc = [&](int pp, double sv) {
@@ -467,6 +479,14 @@ leapfrog_kr(LeapArgsKR a) {
   if constexpr (sizeof(DT) == sizeof(float)) img = reinterpret_cast<const DT*>(a.Df);
   else img = reinterpret_cast<const DT*>(a.D);
   exp_tab_fill(lds);
+  if constexpr (TAB && kImgLds) {  // image after the factor tables (lds_bytes)
+    const int nw = blockDim.x / kWave;
+    DT* simg = reinterpret_cast<DT*>(
+        lds + kExpTab + (size_t)nw * TK::CPW * TK::KMAX * (sizeof(KRStar) / 8) +
+        (size_t)nw * TK::CPW * a.K * 2 * a.side);
+    for (int e = threadIdx.x; e < a.side * a.side; e += blockDim.x) simg[e] = img[e];
+    img = simg;
+  }
   __syncthreads();
   const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
   if (TK::CPW * wave >= a.n_chains) return;
