@@ -1399,6 +1399,39 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   return RHMC_OK;
 }
 
+// Explicit integrators, one star, register-window gradient (rhmc_tiledr.hpp):
+// 28-pixel window, fp32 pixel cache when the image is exact in fp32.
+template <int IMG, typename DT>
+int launch_integrate_tiledr_t(const rhmc_ctx* ctx, const LeapArgsK1& a, int32_t solver,
+                              int f_pos, hipStream_t s) {
+  using TL = TiledR<IMG, 28, DT>;
+  const size_t lds = TL::lds_bytes();
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+  constexpr int W = 4;
+  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  if (solver == RHMC_SOLVER_HMC)
+    hipLaunchKernelGGL((integrate_k1_tiledr<IMG, 28, DT, RHMC_SOLVER_HMC>), grid, block, lds, s,
+                       a, f_pos);
+  else if (solver == RHMC_SOLVER_RHMC_NAIVE)
+    hipLaunchKernelGGL((integrate_k1_tiledr<IMG, 28, DT, RHMC_SOLVER_RHMC_NAIVE>), grid, block,
+                       lds, s, a, f_pos);
+  else
+    hipLaunchKernelGGL((integrate_k1_tiledr<IMG, 28, DT, RHMC_SOLVER_RHMC_LEAPFROG>), grid,
+                       block, lds, s, a, f_pos);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+template <int IMG>
+int launch_integrate_tiledr(const rhmc_ctx* ctx, LeapArgsK1 a, int32_t solver, int f_pos,
+                            hipStream_t s) {
+  if (ctx->img_f32) {
+    a.Df = ctx->d_Df;
+    return launch_integrate_tiledr_t<IMG, float>(ctx, a, solver, f_pos, s);
+  }
+  return launch_integrate_tiledr_t<IMG, double>(ctx, a, solver, f_pos, s);
+}
+
 int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double* d_q,
                      double* d_p, int64_t n, int32_t K, int32_t n_steps, int32_t f_pos,
                      int32_t* d_st, hipStream_t s) {
@@ -1411,6 +1444,32 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   if (rc) return rc;
   if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
   if (n == 0) return RHMC_OK;
+  // one star on a 32/48/64-px image: register-window kernel (RHMC_KERNEL=windowed
+  // keeps the windowed one)
+  const int side = ctx->rows;
+  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_windowed() &&
+      (side == 32 || side == 48 || side == 64) && reg_window_ok(28, a.c.inv_two_sig2)) {
+    LeapArgsK1 t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = nullptr;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n;
+    t.n_steps = n_steps;
+    t.rows = ctx->rows;
+    t.cols = ctx->cols;
+    t.pad = 0;
+    t.c = a.c;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int fp = f_pos != 0;
+    switch (side) {
+      case 32: return launch_integrate_tiledr<32>(ctx, t, solver, fp, s);
+      case 48: return launch_integrate_tiledr<48>(ctx, t, solver, fp, s);
+      default: return launch_integrate_tiledr<64>(ctx, t, solver, fp, s);
+    }
+  }
   if (!window_exact(a.c)) return window_unsupported();  // integrate_win_kernel
   a.q = d_q;
   a.p = d_p;

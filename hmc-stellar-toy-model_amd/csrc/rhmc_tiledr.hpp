@@ -340,4 +340,110 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
   }
 }
 
+// The explicit integrators of single_gym for one star
+// on the register-window gradient: plain HMC, unit metric (sampler_RHMC.py
+// :628-645), explicit RHMC naive (:690-708) and leap_frog (:709-728).
+// dVdq_RHMC's flux slot (:427-446), ((p_f^2 (-H_ff'/H_ff^2)) + H_ff'/H_ff +
+// 2 H_xx'/H_xx)/2, is p_f^2 coef/2 + mterm of the division-lean FluxMetric,
+// and p/H is p A (flux) / p s/g_xx (position).  The metric and gradient at
+// the end of a step are the next step's first ones (same q).
+template <int IMG, int WIN, typename DT, int SOLVER>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+integrate_k1_tiledr(LeapArgsK1 a, int f_pos) {
+  using TL = TiledR<IMG, WIN, DT>;
+  extern __shared__ double lds[];
+  DT* simg = reinterpret_cast<DT*>(lds + kExpTab);
+  const DT* gimg;
+  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
+  else gimg = reinterpret_cast<const DT*>(a.D);
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) {
+    const int r = e / IMG, cc = e - (e / IMG) * IMG;
+    simg[r * TL::P + cc] = gimg[e];
+  }
+  exp_tab_fill(lds);
+  __syncthreads();
+  const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (TL::CPW * wave >= a.n_chains) return;
+  const int lane = lane_id();
+  const int64_t chain = TL::CPW * wave + lane / TL::LPC;
+  const bool real = chain < a.n_chains;            // ragged tail: mirror the wave's first chain
+  const int64_t base = (real ? chain : TL::CPW * wave) * 3;
+
+  double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+  const LeanConsts lc = lean_consts(c);
+  typename TL::Cache cache;
+  TL::init(cache);
+  const double dt = c.dt;
+  unsigned st = 0u;
+  FluxMetric fm{};
+  double gf, gx, gy;
+  auto grad = [&]() {                              // dVdq (:365-425)
+    TL::gradient(lds, simg, cache, f, x, y, c, lc, gf, gx, gy);
+    if (c.use_prior) gf += (SOLVER == RHMC_SOLVER_HMC) ? c.alpha / f : fm.prior;  // :408-409
+  };
+  auto dvdq_rhmc_f = [&](double p_f) { return (p_f * p_f) * fm.coef / 2.0 + fm.mterm; };
+  if constexpr (SOLVER != RHMC_SOLVER_HMC) fm = flux_metric(f, c, lc);
+  grad();
+  for (int step = 0; step < a.n_steps; ++step) {
+    if constexpr (SOLVER == RHMC_SOLVER_HMC) {     // :630-638
+      const double hf = pf - dt * gf / 2.0, hx = px - dt * gx / 2.0, hy = py - dt * gy / 2.0;
+      f = f + dt * hf;
+      x = x + dt * hx;
+      y = y + dt * hy;
+      grad();
+      pf = hf - dt * gf / 2.0;
+      px = hx - dt * gx / 2.0;
+      py = hy - dt * gy / 2.0;
+    } else if constexpr (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :692-705
+      const double ihxx = fm.s * lc.inv_gxx;
+      const double nf = f + (dt * pf) * fm.A, nx = x + (dt * px) * ihxx,
+                   ny = y + (dt * py) * ihxx;
+      const double pf_old = pf;
+      pf = pf - dt * (gf + dvdq_rhmc_f(pf));
+      px = px - dt * gx;
+      py = py - dt * gy;
+      if (f_pos && nf < c.f_lim) {
+        pf = pf_old * -1.0;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+      f = nf;
+      x = nx;
+      y = ny;
+      fm = flux_metric(f, c, lc);
+      grad();
+    } else {                                       // RHMC_SOLVER_RHMC_LEAPFROG, :711-726
+      const double ihxx = fm.s * lc.inv_gxx;
+      const double hf = pf - dt * (gf + dvdq_rhmc_f(pf)) / 2.0;
+      const double hx = px - dt * gx / 2.0, hy = py - dt * gy / 2.0;
+      f = f + (dt * hf) * fm.A;
+      x = x + (dt * hx) * ihxx;
+      y = y + (dt * hy) * ihxx;
+      fm = flux_metric(f, c, lc);
+      grad();
+      pf = hf - dt * (gf + dvdq_rhmc_f(hf)) / 2.0;
+      px = hx - dt * gx / 2.0;
+      py = hy - dt * gy / 2.0;
+      if (f_pos && f < c.f_lim) {
+        pf = hf * -1.0;
+        st |= RHMC_STATUS_REFLECT_F;
+      }
+    }
+  }
+  if ((lane % TL::LPC) == 0 && real) {
+    if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
+          isfinite(py)))
+      st |= RHMC_STATUS_NONFINITE;
+    a.q[base] = f;
+    a.q[base + 1] = x;
+    a.q[base + 2] = y;
+    a.p[base] = pf;
+    a.p[base + 1] = px;
+    a.p[base + 2] = py;
+    if (a.status) a.status[chain] = (int32_t)st;
+  }
+}
+
 }  // namespace rhmc

@@ -37,8 +37,9 @@ def _disassemble(tmp_path):
 
 def test_gfx950_code_object_present_and_hot_kernels_spill_free(tmp_path):
     funcs = _disassemble(tmp_path)
-    leap = [f for f in funcs if "leapfrog" in f]
+    leap = [f for f in funcs if "leapfrog" in f or "integrate_k1" in f]
     assert any("leapfrog_k1_tiled" in f for f in leap)
+    assert sum("integrate_k1_tiledr" in f for f in leap) == 18   # 3 images x 2 DT x 3 solvers
     assert any("leapfrog_tiledk_kernel" in f for f in leap)
     assert any("leapfrog_win_kernel" in f for f in leap)
     for name in leap:
