@@ -1186,8 +1186,8 @@ bool use_tiledrk(const rhmc_ctx* ctx, int K, const Consts& c) {
   return tiledrk_ok(ctx, K, c);
 }
 
-template <typename DT, int SLOTS, bool TAB>
-int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, hipStream_t s) {
+template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
+int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_t s) {
   using TK = TiledRK<DT, SLOTS, TAB>;
   int W = 4;
   while (W > 1 && TK::lds_bytes(W, a.K, a.side) > (size_t)ctx->max_lds / 2) W >>= 1;
@@ -1195,7 +1195,7 @@ int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, hipStream_t s) {
   if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "factor tables exceed LDS");
   const int64_t waves = (a.n_chains + TK::CPW - 1) / TK::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS, TAB>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS, TAB, SOLVER>), grid, block, lds, s, a, f_pos);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -1209,14 +1209,18 @@ bool kr_tables(const rhmc_ctx* ctx, int K) {
   return ctx->rows <= 64 && K <= 16;
 }
 
-int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
+template <int SOLVER = RHMC_SOLVER_IMPLICIT>
+int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, int f_pos, hipStream_t s) {
   const bool f32 = ctx->img_f32;
   if (f32) a.Df = ctx->d_Df;
   if (kr_tables(ctx, a.K))
-    return f32 ? launch_kr_t<float, 1, true>(ctx, a, s) : launch_kr_t<double, 1, true>(ctx, a, s);
+    return f32 ? launch_kr_t<float, 1, true, SOLVER>(ctx, a, f_pos, s)
+               : launch_kr_t<double, 1, true, SOLVER>(ctx, a, f_pos, s);
   if (a.K <= 32)
-    return f32 ? launch_kr_t<float, 1, false>(ctx, a, s) : launch_kr_t<double, 1, false>(ctx, a, s);
-  return f32 ? launch_kr_t<float, 2, false>(ctx, a, s) : launch_kr_t<double, 2, false>(ctx, a, s);
+    return f32 ? launch_kr_t<float, 1, false, SOLVER>(ctx, a, f_pos, s)
+               : launch_kr_t<double, 1, false, SOLVER>(ctx, a, f_pos, s);
+  return f32 ? launch_kr_t<float, 2, false, SOLVER>(ctx, a, f_pos, s)
+             : launch_kr_t<double, 2, false, SOLVER>(ctx, a, f_pos, s);
 }
 
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
@@ -1302,7 +1306,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.side = ctx->rows;
     t.pad = 0;
     t.c = a.c;
-    return launch_kr(ctx, t, s);
+    return launch_kr(ctx, t, 0, s);
   }
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
@@ -1469,6 +1473,27 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
       case 48: return launch_integrate_tiledr<48>(ctx, t, solver, fp, s);
       default: return launch_integrate_tiledr<64>(ctx, t, solver, fp, s);
     }
+  }
+  // many stars: the multi-star register-window kernel (rhmc_tiledrk.hpp)
+  if (use_tiledrk(ctx, K, a.c)) {
+    LeapArgsKR t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = nullptr;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n;
+    t.K = K;
+    t.n_steps = n_steps;
+    t.side = ctx->rows;
+    t.pad = 0;
+    t.c = a.c;
+    HIP_TRY(hipSetDevice(ctx->device));
+    const int fp = f_pos != 0;
+    if (solver == RHMC_SOLVER_HMC) return launch_kr<RHMC_SOLVER_HMC>(ctx, t, fp, s);
+    if (solver == RHMC_SOLVER_RHMC_NAIVE) return launch_kr<RHMC_SOLVER_RHMC_NAIVE>(ctx, t, fp, s);
+    return launch_kr<RHMC_SOLVER_RHMC_LEAPFROG>(ctx, t, fp, s);
   }
   if (!window_exact(a.c)) return window_unsupported();  // integrate_win_kernel
   a.q = d_q;

@@ -467,12 +467,124 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
   }
 }
 
+// n_steps steps of single_gym's explicit integrators for
+// the chain's stars: plain HMC, unit metric (sampler_RHMC.py:628-645), explicit
+// RHMC naive (:690-708) and leap_frog (:709-728), flux wall under f_pos.
+// dVdq_RHMC's flux slot (:427-446) is p_f^2 coef/2 + mterm of the division-
+// lean FluxMetric; p/H is p A (flux) and p s/g_xx (positions).  The gradient
+// and metric at the end of a step are the next step's first ones; the metric
+// is recomputed after each gradient rather than held across it (km_steps).
+template <int SOLVER, int SLOTS, class GRAD>
+__device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x)[SLOTS],
+                                                  double (&y)[SLOTS], double (&pf)[SLOTS],
+                                                  double (&px)[SLOTS], double (&py)[SLOTS],
+                                                  const bool (&own)[SLOTS], KRStar* tab,
+                                                  int n_steps, int f_pos, const Consts& c,
+                                                  const LeanConsts& lc, GRAD grad,
+                                                  unsigned& st) {
+  const double dt = c.dt;
+  FluxMetric fm[SLOTS];
+  double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+  auto metric = [&]() {
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      double fr = f[t];
+      asm volatile("" : "+v"(fr));
+      fm[t] = flux_metric(fr, c, lc);
+    }
+  };
+  auto gradient = [&]() {  // dVdq (:365-425) at the published state
+    grad(x, y, gf, gx, gy);
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t)
+      if (c.use_prior) gf[t] += c.alpha / f[t];     // :408-409
+    // leap_frog needs the metric at the new f right away; naive computes it
+    // at the start of its next step (fewer live registers at SLOTS = 2)
+    if constexpr (SOLVER == RHMC_SOLVER_RHMC_LEAPFROG) metric();
+  };
+  auto dvdq_rhmc_f = [&](int t, double p_f) {
+    return (p_f * p_f) * fm[t].coef / 2.0 + fm[t].mterm;
+  };
+  kr_publish<SLOTS>(tab, f, x, y, own);
+  // naive: the gradient opens each step (nothing of it lives across steps);
+  // HMC / leap_frog carry the end-of-step gradient into the next step
+  if constexpr (SOLVER != RHMC_SOLVER_RHMC_NAIVE) gradient();
+  for (int s = 0; s < n_steps; ++s) {
+    // (p holds the half-step momentum across the gradient: no extra live state)
+    if constexpr (SOLVER == RHMC_SOLVER_HMC) {     // :630-638
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        pf[t] = pf[t] - dt * gf[t] / 2.0;
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+        f[t] = f[t] + dt * pf[t];
+        x[t] = x[t] + dt * px[t];
+        y[t] = y[t] + dt * py[t];
+      }
+      kr_publish<SLOTS>(tab, f, x, y, own);
+      gradient();
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        pf[t] = pf[t] - dt * gf[t] / 2.0;
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+      }
+    } else if constexpr (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :692-705
+      gradient();
+      metric();
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const double ihxx = fm[t].s * lc.inv_gxx;
+        const double nf = f[t] + (dt * pf[t]) * fm[t].A;
+        x[t] = x[t] + (dt * px[t]) * ihxx;
+        y[t] = y[t] + (dt * py[t]) * ihxx;
+        const double pf_old = pf[t];
+        pf[t] = pf[t] - dt * (gf[t] + dvdq_rhmc_f(t, pf[t]));
+        px[t] = px[t] - dt * gx[t];
+        py[t] = py[t] - dt * gy[t];
+        if (f_pos && nf < c.f_lim) {
+          pf[t] = pf_old * -1.0;
+          if (own[t]) st |= RHMC_STATUS_REFLECT_F;
+        }
+        f[t] = nf;
+      }
+      kr_publish<SLOTS>(tab, f, x, y, own);
+    } else {                                       // RHMC_SOLVER_RHMC_LEAPFROG, :711-726
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const double ihxx = fm[t].s * lc.inv_gxx;
+        pf[t] = pf[t] - dt * (gf[t] + dvdq_rhmc_f(t, pf[t])) / 2.0;
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+        f[t] = f[t] + (dt * pf[t]) * fm[t].A;
+        x[t] = x[t] + (dt * px[t]) * ihxx;
+        y[t] = y[t] + (dt * py[t]) * ihxx;
+      }
+      kr_publish<SLOTS>(tab, f, x, y, own);
+      gradient();
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const double hf = pf[t];
+        pf[t] = hf - dt * (gf[t] + dvdq_rhmc_f(t, hf)) / 2.0;
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+        if (f_pos && f[t] < c.f_lim) {
+          pf[t] = hf * -1.0;
+          if (own[t]) st |= RHMC_STATUS_REFLECT_F;
+        }
+      }
+    }
+  }
+}
+
 // Two chains per wave (32 lanes each), W waves per workgroup; two waves per
 // SIMD (<= 256 VGPRs) except the fp64-image / K > 32 variant, which needs more.
-template <typename DT, int SLOTS, bool TAB>
+// SOLVER: RHMC_SOLVER_IMPLICIT = RHMC_single_step (km_steps), else one of the
+// explicit integrators (km_explicit_steps; f_pos = the flux wall).
+template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(sizeof(DT) == 8 && SLOTS == 2 ? 1 : 2)))
-leapfrog_kr(LeapArgsKR a) {
+leapfrog_kr(LeapArgsKR a, int f_pos) {
   using TK = TiledRK<DT, SLOTS, TAB>;
   extern __shared__ double lds[];
   const DT* img;
@@ -521,12 +633,16 @@ leapfrog_kr(LeapArgsKR a) {
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
   const int side = a.side;
-  km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc,
-                  [&](const double (&xs)[SLOTS], const double (&ys)[SLOTS], double (&gf)[SLOTS],
-                      double (&gx)[SLOTS], double (&gy)[SLOTS]) {
-                    TK::gradient(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy);
-                  },
-                  it_p, it_q, st);
+  auto grad = [&](const double (&xs)[SLOTS], const double (&ys)[SLOTS], double (&gf)[SLOTS],
+                  double (&gx)[SLOTS], double (&gy)[SLOTS]) {
+    TK::gradient(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy);
+  };
+  if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT)
+    km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc, grad,
+                    it_p, it_q, st);
+  else
+    km_explicit_steps<SOLVER, SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, f_pos, c, lc,
+                                     grad, st);
 
   unsigned nf = 0u;
 #pragma unroll

@@ -13,4 +13,9 @@ for s in hmc naive leap_frog; do
     > gpurun_out/next/c2_int_$s.json 2> gpurun_out/next/c2_int_$s.err || exit $?
   python3 -c "import json; d=json.load(open('gpurun_out/next/c2_int_$s.json')); print('$s', '%.4g' % d['value'], d['roofline']['kernel_ms'])"
 done
+for s in hmc naive leap_frog; do
+  timeout -k 10 300 python3 bench.py --no-cpu --workload C3 --mode integrate --solver $s --leap 100 --steps 3 --warmup 1 \
+    > gpurun_out/next/c3_int_$s.json 2> gpurun_out/next/c3_int_$s.err || exit $?
+  python3 -c "import json; d=json.load(open('gpurun_out/next/c3_int_$s.json')); print('C3 $s', '%.4g' % d['value'], d['roofline']['kernel_ms'])"
+done
 echo done

@@ -136,3 +136,60 @@ def test_explicit_other_image_sides(gpu_lib, side, name):
         err_q = np.abs(q[k] - qo) / (np.abs(qo) + 1)
         err_p = np.abs(p[k] - po) / (np.abs(po) + 1)
         assert err_q.max() <= 1e-9 and err_p.max() <= 1e-8, (side, name, k, err_q, err_p)
+
+
+# ---- many stars: the multi-star register-window kernel (leapfrog_kr<..., SOLVER>)
+def _star_field(side, K, n_chains, seed):
+    """A C3-style workload (big-sim4 parameters, power-law fluxes) on a
+    side x side image with K stars."""
+    img_rng = np.random.RandomState(seed)
+    rng = np.random.RandomState(seed + 1)
+    par, ftc = workloads.base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
+    ft, xt, yt = workloads._powlaw_stars(img_rng, K, side, ftc)
+    D = workloads._image(side, [(22.5 - 2.5 * np.log10(a / ftc), b, c)
+                                for a, b, c in zip(ft, xt, yt)],
+                         ftc, par["B_count"], par["fwhm_pix"], img_rng)
+    q0 = np.empty((n_chains, 3 * K))
+    q0[:, 0::3] = ft * np.exp(0.1 * rng.randn(n_chains, K))
+    q0[:, 1::3] = xt + 0.5 * rng.randn(n_chains, K)
+    q0[:, 2::3] = yt + 0.5 * rng.randn(n_chains, K)
+    p0 = rng.randn(*q0.shape) * np.sqrt(workloads.metric_diag(q0, par))
+    return workloads.Workload("field", D, q0, p0, par, 0, K, "")
+
+
+@pytest.mark.parametrize("name", SOLVERS)
+@pytest.mark.parametrize("side,K,n_chains", [(48, 10, 16384),   # C3: LDS factor tables
+                                             (48, 20, 37),      # exp path, one star slot
+                                             (64, 40, 5)])      # two star slots per lane
+def test_many_star_explicit_vs_oracle(gpu_lib, name, side, K, n_chains, monkeypatch):
+    capi = gpu_lib
+    wl = workloads.make("C3") if K == 10 else _star_field(side, K, n_chains, 11 + K)
+    params, p0 = _case(wl, name)
+    n = 30
+    ctx = capi.Context(wl.D)
+    try:
+        P = capi.make_params(**params)
+        q, p, st = ctx.integrate(P, _sid(capi, name), wl.q0, p0, n, f_pos=True,
+                                 return_status=True)
+        assert not (st & capi.STATUS_NONFINITE).any()
+        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        qw, pw = ctx.integrate(P, _sid(capi, name), wl.q0, p0, n, f_pos=True)
+        monkeypatch.delenv("RHMC_KERNEL")
+        idx = np.arange(min(n_chains, 13))
+        qs, ps = ctx.integrate(P, _sid(capi, name), wl.q0[idx], p0[idx], n, f_pos=True)
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(qs, q[idx])      # batch invariance (ragged wave)
+    np.testing.assert_array_equal(ps, p[idx])
+    err_q = np.abs(q - qw) / (np.abs(qw) + 1)
+    err_p = np.abs(p - pw) / (np.abs(pw) + 1)
+    assert err_q.max() <= 1e-9 and err_p.max() <= 1e-8, (err_q.max(), err_p.max())
+    par = dict(params)
+    par["rows"], par["cols"] = wl.D.shape
+    m = R.RefModel(wl.D, par)
+    for c in sorted({0, 1, n_chains - 1}):
+        qo, po = _oracle_run(m, name, wl.q0[c], p0[c], n)
+        err_q = np.abs(q[c] - qo) / (np.abs(qo) + 1)
+        err_p = np.abs(p[c] - po) / (np.abs(po) + 1)
+        assert err_q.max() <= 1e-9 and err_p.max() <= 1e-8, (name, K, c, err_q.max(),
+                                                             err_p.max())
