@@ -16,7 +16,7 @@ run c3_mh_5x50 --workload C3 --mode mh --mh-iter 5 --leap 50 --steps 3 --warmup 
 run c2_int_hmc --mode integrate --solver hmc --steps 5 --warmup 1
 run c2_int_naive --mode integrate --solver naive --steps 5 --warmup 1
 run c2_int_leap_frog --mode integrate --solver leap_frog --steps 5 --warmup 1
-run c3_int_leap_frog --workload C3 --mode integrate --solver leap_frog --leap 100 --steps 3 --warmup 1
+for s in hmc naive leap_frog; do run c3_int_$s --workload C3 --mode integrate --solver $s --leap 100 --steps 3 --warmup 1; done
 run c2_datagen --mode datagen --n-real 1000 --steps 10 --warmup 2
 run c5_datagen --workload C5 --mode datagen --n-real 16 --steps 10 --warmup 2
 echo done
