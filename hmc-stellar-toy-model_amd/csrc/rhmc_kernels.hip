@@ -35,6 +35,7 @@
 #include "rhmc_tiledl.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
+#include "rhmc_mhk1.hpp"
 #include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -1346,6 +1347,37 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s);
 
+// One star where launch_leapfrog takes the register-window kernel (28-px
+// window, 32/48/64-px image, fewer chains than the lane-group threshold): the
+// whole MH loop in one launch (rhmc_mhk1.hpp).  RHMC_MH=unfused, or any
+// RHMC_KERNEL override, keeps the four-kernel loop below.
+bool mh_k1_fused(const rhmc_ctx* ctx, const Consts& c, int64_t n) {
+  const char* m = std::getenv("RHMC_MH");
+  if ((m && std::strcmp(m, "unfused") == 0) || std::getenv("RHMC_KERNEL")) return false;
+  const int side = ctx->rows;
+  return !c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
+         reg_window_ok(28, c.inv_two_sig2) && tiledl_lpc(n, nullptr) == 0;
+}
+
+template <int IMG>
+int launch_mh_k1(const rhmc_ctx* ctx, MhK1Args k, hipStream_t s) {
+  const size_t lds16 = TiledR<IMG, 28, float>::lds_bytes();
+  const size_t lds64 = TiledR<IMG, 28, double>::lds_bytes();
+  constexpr int W = 4;
+  const int64_t waves = (k.n + 3) / 4;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  if (ctx->img_f32) {
+    k.Df = ctx->d_Df;
+    if (lds16 > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((mh_k1_tiledr<IMG, 28, float>), grid, block, lds16, s, k);
+  } else {
+    if (lds64 > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((mh_k1_tiledr<IMG, 28, double>), grid, block, lds64, s, k);
+  }
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 // The MH outer loop on device buffers (sampler_RHMC.py:1018-1083): per
 // iteration begin -> n_steps fused leapfrog -> V(q') -> accept, all queued on
 // `s` with no host synchronisation.  `rec` holds device pointers (nullable).
@@ -1357,6 +1389,31 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   if (rc) return rc;
   if (n_iter < 0 || n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter/n_steps < 0");
   if (n == 0 || n_iter == 0) return RHMC_OK;
+  if (K == 1 && mh_k1_fused(ctx, c, n)) {
+    MhK1Args k;
+    k.q = d_q;
+    k.D = ctx->d_D;
+    k.Df = nullptr;
+    k.z = d_z;
+    k.u = d_u;
+    k.q_chain = rec ? rec->q_chain : nullptr;
+    k.E_chain = rec ? rec->E_chain : nullptr;
+    k.V_chain = rec ? rec->V_chain : nullptr;
+    k.T_chain = rec ? rec->T_chain : nullptr;
+    k.accept = rec ? rec->accept : nullptr;
+    k.n = n;
+    k.n_iter = n_iter;
+    k.n_steps = n_steps;
+    k.f_pos = f_pos != 0 ? RHMC_V_FLUX_WALL : 0;
+    k.pad = 0;
+    k.seed = seed;
+    k.c = c;
+    switch (ctx->rows) {
+      case 32: return launch_mh_k1<32>(ctx, k, s);
+      case 48: return launch_mh_k1<48>(ctx, k, s);
+      default: return launch_mh_k1<64>(ctx, k, s);
+    }
+  }
   const size_t sb = (size_t)n * 3 * K * sizeof(double), eb = (size_t)n * sizeof(double);
   const size_t need = 2 * sb + 3 * eb + 256;
   if (need > ctx->mh_scratch_bytes) {

@@ -137,14 +137,10 @@ struct TiledR {
     return swizzle_d<0x13 | ((J << 2) << 5)>(v);
   }
 
-  // The row slice's sums of the chain's dphidq pixel terms: s0 = sum psf s,
-  // s1 = sum psf s dx, s2 = sum psf s dy (s = D/Lambda - 1; every lane of the
-  // chain gets them).
-  static __device__ __forceinline__ void partial(const double* __restrict__ etab,
-                                                 const DT* __restrict__ sD, Cache& k, double f,
-                                                 double x, double y, const Consts& c,
-                                                 const LeanConsts& lc, double& s0, double& s1,
-                                                 double& s2) {
+  // Make the cached window pixels those of the window at (x, y): re-read them
+  // from the LDS image when round(x) or round(y) moved (wave-uniform branch).
+  static __device__ __forceinline__ void ensure(const DT* __restrict__ sD, Cache& k, double x,
+                                                double y) {
     const int m = lane_id() % LPC;
     const int a = m / 4, b = m % 4;
     const bool stay = x >= k.xlo && x < k.xhi && y >= k.ylo && y < k.yhi;
@@ -160,8 +156,17 @@ struct TiledR {
       bounds(x, k.xlo, k.xhi);
       bounds(y, k.ylo, k.yhi);
     }
+  }
+
+  // The PSF factors of this lane's window rows (ex) and columns (ey, with the
+  // 1/(2 pi sigma^2) normalisation): NTR rows + 2 columns evaluated per lane,
+  // then broadcast (utils.py:475-486).
+  static __device__ __forceinline__ void factors(const double* __restrict__ etab, const Cache& k,
+                                                 double x, double y, const LeanConsts& lc,
+                                                 double (&ex)[TR], double (&ey)[TC]) {
+    const int m = lane_id() % LPC;
+    const int a = m / 4, b = m % 4;
     const double r0 = k.r0, c0 = k.c0;
-    // PSF factors: NTR rows + 2 columns per lane, then broadcast.
     double rv[2] = {0.0, 0.0}, cv[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -174,7 +179,6 @@ struct TiledR {
       const double vc = (c0 + ec) - y;
       cv[t] = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
     }
-    double ex[TR], ey[TC];
 #pragma unroll
     for (int i = 0; i < TR; ++i) {
       const double v = rv[i / 4];
@@ -189,6 +193,48 @@ struct TiledR {
             : (j % 4 == 1) ? col_bcast<1>(v)
             : (j % 4 == 2) ? col_bcast<2>(v) : col_bcast<3>(v);
     }
+  }
+
+  // The window's part of the chain's potential V (sampler_RHMC.py:294-302,
+  // Lambda :373-376) relative to the background-only image:
+  //   sum_window (Lambda - B) - D (ln Lambda - ln B).
+  // Outside the window Lambda == B (the window bound), so
+  // V = sum_image (B - D ln B) + this (every lane of the chain gets it).
+  static __device__ __forceinline__ double potential_window(const double* __restrict__ etab,
+                                                            const DT* __restrict__ sD, Cache& k,
+                                                            double f, double x, double y,
+                                                            const Consts& c,
+                                                            const LeanConsts& lc, double lnB) {
+    ensure(sD, k, x, y);
+    double ex[TR], ey[TC];
+    factors(etab, k, x, y, lc, ex, ey);
+    double v = 0.0;
+#pragma unroll
+    for (int i = 0; i < TR; ++i) {
+      const double fe = f * ex[i];
+#pragma unroll
+      for (int j = 0; j < TC; ++j) {
+        const double lam = fma(fe, ey[j], c.B);
+        v += (lam - c.B) - (double)k.d[i * TC + j] * (log(lam) - lnB);
+      }
+    }
+    return group_sum(v);
+  }
+
+  // The row slice's sums of the chain's dphidq pixel terms: s0 = sum psf s,
+  // s1 = sum psf s dx, s2 = sum psf s dy (s = D/Lambda - 1; every lane of the
+  // chain gets them).
+  static __device__ __forceinline__ void partial(const double* __restrict__ etab,
+                                                 const DT* __restrict__ sD, Cache& k, double f,
+                                                 double x, double y, const Consts& c,
+                                                 const LeanConsts& lc, double& s0, double& s1,
+                                                 double& s2) {
+    const int m = lane_id() % LPC;
+    const int a = m / 4, b = m % 4;
+    ensure(sD, k, x, y);
+    const double r0 = k.r0, c0 = k.c0;
+    double ex[TR], ey[TC];
+    factors(etab, k, x, y, lc, ex, ey);
 
     // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
     // pixels (row-major): 1/(l0 l1 l2 l3) by v_rcp_f64 + one Newton step, then
