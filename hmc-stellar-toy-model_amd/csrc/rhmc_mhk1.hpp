@@ -67,7 +67,7 @@ mh_k1_tiledr(MhK1Args a) {
   // star-free image; the window sum corrects it)
   double sd = 0.0;
   for (int e = lane; e < IMG * IMG; e += kWave) sd += (double)simg[(e / IMG) * TL::P + e % IMG];
-  const double lnB = log(c.B);
+  const double lnB = log_pos(c.B);
   const double sum_B = (double)(IMG * IMG) * c.B - lnB * wave_sum(sd);
   double f = a.q[3 * chr], x = a.q[3 * chr + 1], y = a.q[3 * chr + 2];
   const LeanConsts lc = lean_consts(c);
@@ -84,9 +84,34 @@ mh_k1_tiledr(MhK1Args a) {
       v = INFINITY;
     return v;
   };
-  double V0 = potential(f, x, y);
-  for (int it = 0; it < a.n_iter; ++it) {
-    const int64_t r = (int64_t)it * a.n + chr;
+  // One potential evaluation in the code (it is the bulk of the kernel's
+  // code): pass it = -1 evaluates V(q) of the starting state, pass it >= 0
+  // evaluates V(q') of iteration it's proposal and decides it, then the next
+  // iteration is drawn and integrated.
+  double V0 = 0.0, E0 = 0.0;
+  double f1 = f, x1 = x, y1 = y, pf = 0.0, px = 0.0, py = 0.0;
+  for (int it = -1; it < a.n_iter; ++it) {
+    const double V1 = potential(f1, x1, y1);
+    if (it < 0) {
+      V0 = V1;
+    } else {
+      const int64_t r = (int64_t)it * a.n + chr;
+      const double q3p[3] = {f1, x1, y1};
+      const double p3p[3] = {pf, px, py};
+      const double dE = (V1 + kinetic(q3p, p3p, 1, c)) - E0;
+      const double uu = a.u ? a.u[r] : philox_uniform(a.seed, chr, it);
+      const bool acc = (dE < 0.0) || (log(uu) < -dE);  // :1076
+      if (acc) {
+        f = f1;
+        x = x1;
+        y = y1;
+        V0 = V1;
+      }
+      if (writer && a.accept) a.accept[r] = acc ? 1 : 0;
+    }
+    const int nx = it + 1;
+    if (nx == a.n_iter) break;
+    const int64_t r = (int64_t)nx * a.n + chr;
     double hff, hxx;
     metric_pair(f, c, hff, hxx);
     double z0, z1, z2;
@@ -95,15 +120,17 @@ mh_k1_tiledr(MhK1Args a) {
       z1 = a.z[3 * r + 1];
       z2 = a.z[3 * r + 2];
     } else {
-      z0 = philox_normal(a.seed, chr, it, 0);
-      z1 = philox_normal(a.seed, chr, it, 1);
-      z2 = philox_normal(a.seed, chr, it, 2);
+      z0 = philox_normal(a.seed, chr, nx, 0);
+      z1 = philox_normal(a.seed, chr, nx, 1);
+      z2 = philox_normal(a.seed, chr, nx, 2);
     }
-    double pf = z0 * sqrt(hff), px = z1 * sqrt(hxx), py = z2 * sqrt(hxx);  // :1022
+    pf = z0 * sqrt(hff);                           // :1022
+    px = z1 * sqrt(hxx);
+    py = z2 * sqrt(hxx);
     const double q3[3] = {f, x, y};
     const double p3[3] = {pf, px, py};
     const double T0 = kinetic(q3, p3, 1, c);
-    const double E0 = V0 + T0;
+    E0 = V0 + T0;
     if (writer) {
       if (a.q_chain) {
         a.q_chain[3 * r] = f;
@@ -114,7 +141,9 @@ mh_k1_tiledr(MhK1Args a) {
       if (a.T_chain) a.T_chain[r] = T0;
       if (a.E_chain) a.E_chain[r] = E0;
     }
-    double f1 = f, x1 = x, y1 = y;
+    f1 = f;
+    x1 = x;
+    y1 = y;
     int it_p = 0, it_q = 0;
     unsigned st = 0u;
     k1_steps(f1, x1, y1, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
@@ -122,19 +151,6 @@ mh_k1_tiledr(MhK1Args a) {
                TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
              },
              it_p, it_q, st);
-    const double V1 = potential(f1, x1, y1);
-    const double q3p[3] = {f1, x1, y1};
-    const double p3p[3] = {pf, px, py};
-    const double dE = (V1 + kinetic(q3p, p3p, 1, c)) - E0;
-    const double uu = a.u ? a.u[r] : philox_uniform(a.seed, chr, it);
-    const bool acc = (dE < 0.0) || (log(uu) < -dE);  // :1076
-    if (acc) {
-      f = f1;
-      x = x1;
-      y = y1;
-      V0 = V1;
-    }
-    if (writer && a.accept) a.accept[r] = acc ? 1 : 0;
   }
   if (writer) {
     a.q[3 * ch] = f;

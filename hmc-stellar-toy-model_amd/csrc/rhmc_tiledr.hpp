@@ -200,6 +200,7 @@ struct TiledR {
   //   sum_window (Lambda - B) - D (ln Lambda - ln B).
   // Outside the window Lambda == B (the window bound), so
   // V = sum_image (B - D ln B) + this (every lane of the chain gets it).
+  // lnB must be log_pos(B) (the same log on both sides of the difference).
   static __device__ __forceinline__ double potential_window(const double* __restrict__ etab,
                                                             const DT* __restrict__ sD, Cache& k,
                                                             double f, double x, double y,
@@ -215,7 +216,7 @@ struct TiledR {
 #pragma unroll
       for (int j = 0; j < TC; ++j) {
         const double lam = fma(fe, ey[j], c.B);
-        v += (lam - c.B) - (double)k.d[i * TC + j] * (log(lam) - lnB);
+        v += (lam - c.B) - (double)k.d[i * TC + j] * (log_pos(lam) - lnB);
       }
     }
     return group_sum(v);

@@ -1,0 +1,13 @@
+#!/bin/bash
+# A/B of the default bench between the in-tree library and build/variants/lib_$1.so,
+# alternating on one box.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+mkdir -p gpurun_out/ab
+V=$1; shift
+for r in 1 2 3; do
+  for lib in new $V; do
+    if [ $lib = new ]; then L=hmc-stellar-toy-model_amd/librhmc.so; else L=build/variants/lib_$lib.so; fi
+    RHMC_LIB=$L timeout -k 10 120 python3 bench.py --no-cpu --steps 20 --warmup 3 "$@" > gpurun_out/ab/$lib.$r.json || exit $?
+    python3 -c "import json; d=json.load(open('gpurun_out/ab/$lib.$r.json')); print('$lib $r', '%.4g' % d['value'], '%.4f' % d['roofline']['kernel_ms'])"
+  done
+done
