@@ -432,18 +432,35 @@ integrate_k1_tiledr(LeapArgsK1 a, int f_pos) {
     if (c.use_prior) gf += (SOLVER == RHMC_SOLVER_HMC) ? c.alpha / f : fm.prior;  // :408-409
   };
   auto dvdq_rhmc_f = [&](double p_f) { return (p_f * p_f) * fm.coef / 2.0 + fm.mterm; };
-  if constexpr (SOLVER != RHMC_SOLVER_HMC) fm = flux_metric(f, c, lc);
-  grad();
-  for (int step = 0; step < a.n_steps; ++step) {
-    if constexpr (SOLVER == RHMC_SOLVER_HMC) {     // :630-638
-      const double hf = pf - dt * gf / 2.0, hx = px - dt * gx / 2.0, hy = py - dt * gy / 2.0;
-      f = f + dt * hf;
-      x = x + dt * hx;
-      y = y + dt * hy;
-      grad();
-      pf = hf - dt * gf / 2.0;
-      px = hx - dt * gx / 2.0;
-      py = hy - dt * gy / 2.0;
+  // One gradient call site: pass s closes step s - 1 and opens step s (p holds
+  // the half-step momentum across the gradient); naive's gradient opens its step.
+  for (int s = 0;; ++s) {
+    if constexpr (SOLVER != RHMC_SOLVER_HMC) fm = flux_metric(f, c, lc);
+    grad();
+    if (s > 0) {
+      if constexpr (SOLVER == RHMC_SOLVER_HMC) {   // :630-638
+        pf = pf - dt * gf / 2.0;
+      } else if constexpr (SOLVER == RHMC_SOLVER_RHMC_LEAPFROG) {  // :711-726
+        const double hf = pf;
+        pf = hf - dt * (gf + dvdq_rhmc_f(hf)) / 2.0;
+        if (f_pos && f < c.f_lim) {
+          pf = hf * -1.0;
+          st |= RHMC_STATUS_REFLECT_F;
+        }
+      }
+      if constexpr (SOLVER != RHMC_SOLVER_RHMC_NAIVE) {
+        px = px - dt * gx / 2.0;
+        py = py - dt * gy / 2.0;
+      }
+    }
+    if (s == a.n_steps) break;
+    if constexpr (SOLVER == RHMC_SOLVER_HMC) {
+      pf = pf - dt * gf / 2.0;
+      px = px - dt * gx / 2.0;
+      py = py - dt * gy / 2.0;
+      f = f + dt * pf;
+      x = x + dt * px;
+      y = y + dt * py;
     } else if constexpr (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :692-705
       const double ihxx = fm.s * lc.inv_gxx;
       const double nf = f + (dt * pf) * fm.A, nx = x + (dt * px) * ihxx,
@@ -459,24 +476,14 @@ integrate_k1_tiledr(LeapArgsK1 a, int f_pos) {
       f = nf;
       x = nx;
       y = ny;
-      fm = flux_metric(f, c, lc);
-      grad();
-    } else {                                       // RHMC_SOLVER_RHMC_LEAPFROG, :711-726
+    } else {
       const double ihxx = fm.s * lc.inv_gxx;
-      const double hf = pf - dt * (gf + dvdq_rhmc_f(pf)) / 2.0;
-      const double hx = px - dt * gx / 2.0, hy = py - dt * gy / 2.0;
-      f = f + (dt * hf) * fm.A;
-      x = x + (dt * hx) * ihxx;
-      y = y + (dt * hy) * ihxx;
-      fm = flux_metric(f, c, lc);
-      grad();
-      pf = hf - dt * (gf + dvdq_rhmc_f(hf)) / 2.0;
-      px = hx - dt * gx / 2.0;
-      py = hy - dt * gy / 2.0;
-      if (f_pos && f < c.f_lim) {
-        pf = hf * -1.0;
-        st |= RHMC_STATUS_REFLECT_F;
-      }
+      pf = pf - dt * (gf + dvdq_rhmc_f(pf)) / 2.0;
+      px = px - dt * gx / 2.0;
+      py = py - dt * gy / 2.0;
+      f = f + (dt * pf) * fm.A;
+      x = x + (dt * px) * ihxx;
+      y = y + (dt * py) * ihxx;
     }
   }
   if ((lane % TL::LPC) == 0 && real) {

@@ -506,30 +506,9 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
     return (p_f * p_f) * fm[t].coef / 2.0 + fm[t].mterm;
   };
   kr_publish<SLOTS>(tab, f, x, y, own);
-  // naive: the gradient opens each step (nothing of it lives across steps);
-  // HMC / leap_frog carry the end-of-step gradient into the next step
-  if constexpr (SOLVER != RHMC_SOLVER_RHMC_NAIVE) gradient();
-  for (int s = 0; s < n_steps; ++s) {
-    // (p holds the half-step momentum across the gradient: no extra live state)
-    if constexpr (SOLVER == RHMC_SOLVER_HMC) {     // :630-638
-#pragma unroll
-      for (int t = 0; t < SLOTS; ++t) {
-        pf[t] = pf[t] - dt * gf[t] / 2.0;
-        px[t] = px[t] - dt * gx[t] / 2.0;
-        py[t] = py[t] - dt * gy[t] / 2.0;
-        f[t] = f[t] + dt * pf[t];
-        x[t] = x[t] + dt * px[t];
-        y[t] = y[t] + dt * py[t];
-      }
-      kr_publish<SLOTS>(tab, f, x, y, own);
-      gradient();
-#pragma unroll
-      for (int t = 0; t < SLOTS; ++t) {
-        pf[t] = pf[t] - dt * gf[t] / 2.0;
-        px[t] = px[t] - dt * gx[t] / 2.0;
-        py[t] = py[t] - dt * gy[t] / 2.0;
-      }
-    } else if constexpr (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :692-705
+  if constexpr (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :692-705
+    // the gradient opens each step (nothing of it lives across steps)
+    for (int s = 0; s < n_steps; ++s) {
       gradient();
       metric();
 #pragma unroll
@@ -549,9 +528,42 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
         f[t] = nf;
       }
       kr_publish<SLOTS>(tab, f, x, y, own);
-    } else {                                       // RHMC_SOLVER_RHMC_LEAPFROG, :711-726
+    }
+    return;
+  }
+  // HMC (:630-638) / leap_frog (:711-726): one gradient call site (code size:
+  // the gradient is most of the kernel), pass s closes step s - 1 and opens
+  // step s; p holds the half-step momentum across the gradient.
+  for (int s = 0;; ++s) {
+    gradient();
+    if (s > 0) {
 #pragma unroll
       for (int t = 0; t < SLOTS; ++t) {
+        if constexpr (SOLVER == RHMC_SOLVER_HMC) {
+          pf[t] = pf[t] - dt * gf[t] / 2.0;
+        } else {
+          const double hf = pf[t];
+          pf[t] = hf - dt * (gf[t] + dvdq_rhmc_f(t, hf)) / 2.0;
+          if (f_pos && f[t] < c.f_lim) {
+            pf[t] = hf * -1.0;
+            if (own[t]) st |= RHMC_STATUS_REFLECT_F;
+          }
+        }
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+      }
+    }
+    if (s == n_steps) break;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      if constexpr (SOLVER == RHMC_SOLVER_HMC) {
+        pf[t] = pf[t] - dt * gf[t] / 2.0;
+        px[t] = px[t] - dt * gx[t] / 2.0;
+        py[t] = py[t] - dt * gy[t] / 2.0;
+        f[t] = f[t] + dt * pf[t];
+        x[t] = x[t] + dt * px[t];
+        y[t] = y[t] + dt * py[t];
+      } else {
         const double ihxx = fm[t].s * lc.inv_gxx;
         pf[t] = pf[t] - dt * (gf[t] + dvdq_rhmc_f(t, pf[t])) / 2.0;
         px[t] = px[t] - dt * gx[t] / 2.0;
@@ -560,20 +572,8 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
         x[t] = x[t] + (dt * px[t]) * ihxx;
         y[t] = y[t] + (dt * py[t]) * ihxx;
       }
-      kr_publish<SLOTS>(tab, f, x, y, own);
-      gradient();
-#pragma unroll
-      for (int t = 0; t < SLOTS; ++t) {
-        const double hf = pf[t];
-        pf[t] = hf - dt * (gf[t] + dvdq_rhmc_f(t, hf)) / 2.0;
-        px[t] = px[t] - dt * gx[t] / 2.0;
-        py[t] = py[t] - dt * gy[t] / 2.0;
-        if (f_pos && f[t] < c.f_lim) {
-          pf[t] = hf * -1.0;
-          if (own[t]) st |= RHMC_STATUS_REFLECT_F;
-        }
-      }
     }
+    kr_publish<SLOTS>(tab, f, x, y, own);
   }
 }
 
