@@ -1115,8 +1115,50 @@ int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
 }
 
 // V (and optionally T) of n chains on device buffers, async on `s`.
+template <int IMG>
+int launch_energy_k1(const rhmc_ctx* ctx, EnergyK1Args k, hipStream_t s) {
+  constexpr int W = 4;
+  const int64_t waves = (k.n + 3) / 4;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  if (ctx->img_f32) {
+    k.Df = ctx->d_Df;
+    const size_t lds = TiledR<IMG, 28, float>::lds_bytes();
+    if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((energy_k1_tiledr<IMG, float>), grid, block, lds, s, k);
+  } else {
+    const size_t lds = TiledR<IMG, 28, double>::lds_bytes();
+    if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((energy_k1_tiledr<IMG, double>), grid, block, lds, s, k);
+  }
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const double* d_p,
                   double* d_V, double* d_T, int64_t n, int K, int f_pos, hipStream_t s) {
+  // one star on a 32/48/64-px image: the register-window energy kernel
+  // (rhmc_mhk1.hpp); any RHMC_KERNEL override keeps the per-wave kernels
+  const int side = ctx->rows;
+  if (K == 1 && !c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
+      reg_window_ok(28, c.inv_two_sig2) && !std::getenv("RHMC_KERNEL")) {
+    if (n == 0) return RHMC_OK;
+    EnergyK1Args k;
+    k.q = d_q;
+    k.p = d_p;
+    k.V = d_V;
+    k.T = d_T;
+    k.D = ctx->d_D;
+    k.Df = nullptr;
+    k.n = n;
+    k.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
+    k.pad = 0;
+    k.c = c;
+    switch (side) {
+      case 32: return launch_energy_k1<32>(ctx, k, s);
+      case 48: return launch_energy_k1<48>(ctx, k, s);
+      default: return launch_energy_k1<64>(ctx, k, s);
+    }
+  }
   EnergyArgs a;
   a.c = c;
   size_t lds;

@@ -38,23 +38,61 @@ struct MhK1Args {
   Consts c;
 };
 
-template <int IMG, int WIN, typename DT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
-mh_k1_tiledr(MhK1Args a) {
-  using TL = TiledR<IMG, WIN, DT>;
-  extern __shared__ double lds[];
+// Workgroup prologue of the one-star register-window kernels: the image into
+// LDS (row pitch TL::P) and the exp table.
+template <class TL, typename DT>
+__device__ __forceinline__ DT* k1_stage_image(double* lds, const DT* gimg) {
+  constexpr int IMG = TL::P - 1;
   DT* simg = reinterpret_cast<DT*>(lds + kExpTab);
-  const DT* gimg;
-  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
-  else gimg = reinterpret_cast<const DT*>(a.D);
-  const Consts& c = a.c;
-  const int W = blockDim.x / kWave;
   for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) {
     const int r = e / IMG, cc = e - (e / IMG) * IMG;
     simg[r * TL::P + cc] = gimg[e];
   }
   exp_tab_fill(lds);
   __syncthreads();
+  return simg;
+}
+
+// sum over the image of B - D ln B = IMG^2 B - ln B sum D (the V of a
+// star-free image; the window sum corrects it), lnB = log_pos(B).  Wave-wide.
+template <class TL, typename DT>
+__device__ __forceinline__ double k1_background_V(const DT* simg, double B, double lnB) {
+  constexpr int IMG = TL::P - 1;
+  double sd = 0.0;
+  for (int e = lane_id(); e < IMG * IMG; e += kWave) sd += (double)simg[(e / IMG) * TL::P + e % IMG];
+  return (double)(IMG * IMG) * B - lnB * wave_sum(sd);
+}
+
+// V(q) of one star (sampler_RHMC.py:294-330): the background V plus the
+// window's correction plus the prior, infinite outside the support (f_pos:
+// RHMC_V_FLUX_WALL / RHMC_V_NO_POSCHECK).  The window sum is evaluated either
+// way (no divergence inside a chain's lane group).
+template <class TL, typename DT>
+__device__ __forceinline__ double k1_potential(const double* lds, const DT* simg,
+                                               typename TL::Cache& cache, double f, double x,
+                                               double y, int f_pos, double sum_B, double lnB,
+                                               const Consts& c, const LeanConsts& lc) {
+  constexpr int IMG = TL::P - 1;
+  double v = sum_B + TL::potential_window(lds, simg, cache, f, x, y, c, lc, lnB);
+  if (c.use_prior) v += c.alpha * log(f) + c.vprior;     // :326, :329-330
+  if (((f_pos & RHMC_V_FLUX_WALL) && f < c.f_lim) ||
+      (!(f_pos & RHMC_V_NO_POSCHECK) &&
+       (x < -1.0 || x > (double)(IMG + 1) || y < -1.0 || y > (double)(IMG + 1))))
+    v = INFINITY;
+  return v;
+}
+
+template <int IMG, int WIN, typename DT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+mh_k1_tiledr(MhK1Args a) {
+  using TL = TiledR<IMG, WIN, DT>;
+  extern __shared__ double lds[];
+  const DT* gimg;
+  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
+  else gimg = reinterpret_cast<const DT*>(a.D);
+  const DT* simg = k1_stage_image<TL>(lds, gimg);
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
   const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (TL::CPW * wave >= a.n) return;
   const int lane = lane_id();
@@ -63,26 +101,14 @@ mh_k1_tiledr(MhK1Args a) {
   const int64_t chr = real ? ch : TL::CPW * wave;
   const bool writer = real && (lane % TL::LPC) == 0;
 
-  // sum over the image of B - D ln B = IMG^2 B - ln B sum D (the V of a
-  // star-free image; the window sum corrects it)
-  double sd = 0.0;
-  for (int e = lane; e < IMG * IMG; e += kWave) sd += (double)simg[(e / IMG) * TL::P + e % IMG];
   const double lnB = log_pos(c.B);
-  const double sum_B = (double)(IMG * IMG) * c.B - lnB * wave_sum(sd);
+  const double sum_B = k1_background_V<TL>(simg, c.B, lnB);
   double f = a.q[3 * chr], x = a.q[3 * chr + 1], y = a.q[3 * chr + 2];
   const LeanConsts lc = lean_consts(c);
   typename TL::Cache cache;
   TL::init(cache);
-  // V(q) (:294-330): infinite outside the support, else window sum + prior
-  // (the window sum is evaluated either way: no divergence inside a wave)
   auto potential = [&](double f_, double x_, double y_) {
-    double v = sum_B + TL::potential_window(lds, simg, cache, f_, x_, y_, c, lc, lnB);
-    if (c.use_prior) v += c.alpha * log(f_) + c.vprior;   // :326, :329-330
-    if (((a.f_pos & RHMC_V_FLUX_WALL) && f_ < c.f_lim) ||
-        (!(a.f_pos & RHMC_V_NO_POSCHECK) &&
-         (x_ < -1.0 || x_ > (double)(IMG + 1) || y_ < -1.0 || y_ > (double)(IMG + 1))))
-      v = INFINITY;
-    return v;
+    return k1_potential<TL>(lds, simg, cache, f_, x_, y_, a.f_pos, sum_B, lnB, c, lc);
   };
   // One potential evaluation in the code (it is the bulk of the kernel's
   // code): pass it = -1 evaluates V(q) of the starting state, pass it >= 0
@@ -157,6 +183,57 @@ mh_k1_tiledr(MhK1Args a) {
     a.q[3 * ch + 1] = x;
     a.q[3 * ch + 2] = y;
   }
+}
+
+// V and T of one-star chains (the energy kernel's job, sampler_RHMC.py
+// :294-363) on the register-window layout: 16 lanes per chain, V from the
+// window correction (784 logs per chain instead of the image's 2304).
+struct EnergyK1Args {
+  const double* q;
+  const double* p;   // nullable: no T
+  double* V;         // nullable: no V
+  double* T;
+  const double* D;
+  const float* Df;
+  int64_t n;
+  int f_pos, pad;
+  Consts c;
+};
+
+template <int IMG, typename DT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+energy_k1_tiledr(EnergyK1Args a) {
+  using TL = TiledR<IMG, 28, DT>;
+  extern __shared__ double lds[];
+  const DT* gimg;
+  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
+  else gimg = reinterpret_cast<const DT*>(a.D);
+  const DT* simg = k1_stage_image<TL>(lds, gimg);
+  const Consts& c = a.c;
+  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  if (TL::CPW * wave >= a.n) return;
+  const int lane = lane_id();
+  const int64_t ch = TL::CPW * wave + lane / TL::LPC;
+  const bool real = ch < a.n;                      // ragged tail: mirror the wave's first chain
+  const int64_t chr = real ? ch : TL::CPW * wave;
+  const bool writer = real && (lane % TL::LPC) == 0;
+  const double f = a.q[3 * chr], x = a.q[3 * chr + 1], y = a.q[3 * chr + 2];
+  if (a.T) {  // T(p, H(q)) (:353-363), the energy kernel's expression
+    const double pf = a.p[3 * chr], px = a.p[3 * chr + 1], py = a.p[3 * chr + 2];
+    double hff, hxx;
+    metric_pair(f, c, hff, hxx);
+    const double t1 = pf * pf / hff + px * px / hxx + py * py / hxx;
+    const double t2 = log(fabs(hff)) + log(fabs(hxx)) + log(fabs(hxx));
+    if (writer) a.T[ch] = (t1 + t2) / 2.0;
+  }
+  if (!a.V) return;
+  const double lnB = log_pos(c.B);
+  const double sum_B = k1_background_V<TL>(simg, c.B, lnB);
+  const LeanConsts lc = lean_consts(c);
+  typename TL::Cache cache;
+  TL::init(cache);
+  const double v = k1_potential<TL>(lds, simg, cache, f, x, y, a.f_pos, sum_B, lnB, c, lc);
+  if (writer) a.V[ch] = v;
 }
 
 }  // namespace rhmc
