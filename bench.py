@@ -170,11 +170,13 @@ def main():
                     help="total chains split over the ranks (strong scaling, e.g. C4 = 2^20)")
     ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "datagen"),
+    ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "hmc_random", "datagen"),
                     default="leapfrog",
                     help="mh: whole MH iterations on device (momentum draw, V+T, accept; "
                          "Philox RNG); one bench step = --mh-iter iterations of --leap steps. "
                          "integrate: --solver's explicit integrator (rhmc_integrate). "
+                         "hmc_random: samplers.HMC_random trajectories of --leap steps "
+                         "(rhmc_hmc_random). "
                          "datagen: --n-real Poisson realisations of the workload's model "
                          "image (rhmc_gen_image)")
     ap.add_argument("--mh-iter", type=int, default=10)
@@ -240,6 +242,17 @@ def main():
         def launch():
             ctx.integrate_device(P, solver, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
                                  f_pos=True, status_ptr=st.data_ptr(), stream=stream.cuda_stream)
+    elif args.mode == "hmc_random":
+        # samplers.HMC_random trajectories: unit mass, per-coordinate step
+        # (flux 2.0, positions 0.02), every chain `leap` steps
+        dtv = torch.tensor([2.0, 0.02, 0.02] * wl.K, dtype=torch.float64, device=dev)
+        nst = torch.full((wl.n_chains,), leap, dtype=torch.int32, device=dev)
+        p.normal_(generator=torch.Generator(device=dev).manual_seed(7 + rank))
+
+        def launch():
+            ctx.hmc_random_device(P, dtv.data_ptr(), q.data_ptr(), p.data_ptr(), nst.data_ptr(),
+                                  wl.n_chains, wl.K, status_ptr=st.data_ptr(),
+                                  stream=stream.cuda_stream)
     else:
         def launch():
             ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), wl.n_chains, wl.K, leap,
@@ -311,7 +324,8 @@ def main():
                    "chains_per_gpu": wl.n_chains, "total_chains": total_chains,
                    "image": list(wl.D.shape), "K": wl.K,
                    "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
-                   "solver": args.solver if args.mode == "integrate" else "implicit",
+                   "solver": (args.solver if args.mode == "integrate" else
+                              "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

@@ -1621,6 +1621,26 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   return RHMC_OK;
 }
 
+template <int IMG>
+int launch_hmc_random_k1(const rhmc_ctx* ctx, LeapArgsK1 t, const double* d_dt,
+                         const int32_t* d_steps, hipStream_t s) {
+  constexpr int W = 4;
+  const int64_t waves = (t.n_chains + 3) / 4;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  if (ctx->img_f32) {
+    t.Df = ctx->d_Df;
+    const size_t lds = TiledR<IMG, 28, float>::lds_bytes();
+    if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((hmc_random_k1_tiledr<IMG, float>), grid, block, lds, s, t, d_dt, d_steps);
+  } else {
+    const size_t lds = TiledR<IMG, 28, double>::lds_bytes();
+    if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
+    hipLaunchKernelGGL((hmc_random_k1_tiledr<IMG, double>), grid, block, lds, s, t, d_dt, d_steps);
+  }
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, double* d_q,
                       double* d_p, const int32_t* d_steps, int64_t n, int32_t K, int32_t* d_st,
                       hipStream_t s) {
@@ -1629,6 +1649,31 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   if (rc) return rc;
   if (n == 0) return RHMC_OK;
   if (!d_dt || !d_steps) return fail(RHMC_ERR_ARG, "dt/steps is NULL");
+  // one star on a 32/48/64-px image: register-window kernel (any RHMC_KERNEL
+  // override keeps the windowed one)
+  const int side = ctx->rows;
+  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
+      reg_window_ok(28, a.c.inv_two_sig2) && !std::getenv("RHMC_KERNEL")) {
+    LeapArgsK1 t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = nullptr;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n;
+    t.n_steps = 0;
+    t.rows = ctx->rows;
+    t.cols = ctx->cols;
+    t.pad = 0;
+    t.c = a.c;
+    HIP_TRY(hipSetDevice(ctx->device));
+    switch (side) {
+      case 32: return launch_hmc_random_k1<32>(ctx, t, d_dt, d_steps, s);
+      case 48: return launch_hmc_random_k1<48>(ctx, t, d_dt, d_steps, s);
+      default: return launch_hmc_random_k1<64>(ctx, t, d_dt, d_steps, s);
+    }
+  }
   if (!window_exact(a.c)) return window_unsupported();  // windowed gradient
   a.q = d_q;
   a.p = d_p;

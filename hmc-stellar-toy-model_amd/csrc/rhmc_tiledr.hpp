@@ -500,4 +500,87 @@ integrate_k1_tiledr(LeapArgsK1 a, int f_pos) {
   }
 }
 
+// samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552) for one
+// star on the register-window gradient: unit-mass leapfrog with the step vector
+// dtv[3], the chain's length steps[chain] >= 1 (wave lanes of finished chains
+// idle; every cross-lane exchange stays inside a chain's 16 lanes), the flux wall
+// at c.f_lim with the reference's quirks (hmc_random_win_kernel: the flip mask
+// is never cleared; a trajectory whose last step flipped keeps its starting
+// momentum, status RHMC_STATUS_REFLECT_F).  dVdq without the metric (:365-425).
+template <int IMG, typename DT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1)))
+hmc_random_k1_tiledr(LeapArgsK1 a, const double* __restrict__ dtv,
+                     const int32_t* __restrict__ steps) {
+  using TL = TiledR<IMG, 28, DT>;
+  extern __shared__ double lds[];
+  DT* simg = reinterpret_cast<DT*>(lds + kExpTab);
+  const DT* gimg;
+  if constexpr (sizeof(DT) == sizeof(float)) gimg = reinterpret_cast<const DT*>(a.Df);
+  else gimg = reinterpret_cast<const DT*>(a.D);
+  const Consts& c = a.c;
+  const int W = blockDim.x / kWave;
+  for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) {
+    const int r = e / IMG, cc = e - (e / IMG) * IMG;
+    simg[r * TL::P + cc] = gimg[e];
+  }
+  exp_tab_fill(lds);
+  __syncthreads();
+  const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  if (TL::CPW * wave >= a.n_chains) return;
+  const int lane = lane_id();
+  const int64_t chain = TL::CPW * wave + lane / TL::LPC;
+  const bool real = chain < a.n_chains;            // ragged tail: mirror the wave's first chain
+  const int64_t cr = real ? chain : TL::CPW * wave;
+  const int64_t base = cr * 3;
+  double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
+  const double dtf = dtv[0], dtx = dtv[1], dty = dtv[2];
+  const LeanConsts lc = lean_consts(c);
+  typename TL::Cache cache;
+  TL::init(cache);
+  double gf, gx, gy;
+  auto grad = [&]() {                              // dVdq (:365-425)
+    TL::gradient(lds, simg, cache, f, x, y, c, lc, gf, gx, gy);
+    if (c.use_prior) gf += c.alpha / f;            // :408-409
+  };
+  grad();
+  double hf = pf - dtf * gf / 2.0, hx = px - dtx * gx / 2.0,  // :519
+         hy = py - dty * gy / 2.0;
+  bool iflip = false, flip = false;
+  const int n = steps[cr];
+  for (int t = 0; t < n; ++t) {
+    f = f + dtf * hf;                                          // :523
+    x = x + dtx * hx;
+    y = y + dty * hy;
+    flip = f < c.f_lim;                                        // :526-529 (one star)
+    iflip = iflip || flip;
+    grad();
+    const double kept = -hf;                                   // :531
+    hf = hf - dtf * gf;                                        // :532, :535
+    hx = hx - dtx * gx;
+    hy = hy - dty * gy;
+    if (flip && iflip) hf = kept;                              // :533
+  }
+  unsigned st = 0u;
+  if (flip) {
+    st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
+  } else {                        // :551-552, dVdq at the same q as the last step
+    pf = hf + dtf * gf / 2.0;
+    px = hx + dtx * gx / 2.0;
+    py = hy + dty * gy / 2.0;
+  }
+  if ((lane % TL::LPC) == 0 && real) {
+    if (!(isfinite(f) && isfinite(x) && isfinite(y) && isfinite(pf) && isfinite(px) &&
+          isfinite(py)))
+      st |= RHMC_STATUS_NONFINITE;
+    a.q[base] = f;
+    a.q[base + 1] = x;
+    a.q[base + 2] = y;
+    a.p[base] = pf;
+    a.p[base + 1] = px;
+    a.p[base + 2] = py;
+    if (a.status) a.status[chain] = (int32_t)st;
+  }
+}
+
 }  // namespace rhmc

@@ -349,6 +349,16 @@ class Context:
             q2, p2, st = q2[0], p2[0], st[0]
         return (q2, p2, st) if return_status else (q2, p2)
 
+    def hmc_random_device(self, params, dt_ptr, q_ptr, p_ptr, steps_ptr, n_chains, K,
+                          status_ptr=None, stream=None):
+        """Device-pointer rhmc_hmc_random (asynchronous on `stream`)."""
+        _check(_lib.rhmc_hmc_random_device(self._h, ctypes.byref(params),
+                                           ctypes.c_void_p(dt_ptr), ctypes.c_void_p(q_ptr),
+                                           ctypes.c_void_p(p_ptr), ctypes.c_void_p(steps_ptr),
+                                           int(n_chains), int(K),
+                                           ctypes.c_void_p(status_ptr or 0),
+                                           ctypes.c_void_p(stream or 0)))
+
     def integrate_device(self, params, solver, q_ptr, p_ptr, n_chains, K, n_steps, f_pos=False,
                          status_ptr=None, stream=None):
         """Device-pointer rhmc_integrate (asynchronous on `stream`)."""

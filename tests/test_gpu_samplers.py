@@ -114,3 +114,57 @@ def test_HMC_random_batched(gpu_lib):
                 qt[c] = qn
             assert np.abs(g.q_chain[c, i] - qt[c]).max() / (np.abs(qt[c]).max() + 1) <= 1e-10
     assert p_init.shape == (n, d)
+
+
+@pytest.mark.parametrize("side,wall", [(48, False), (48, True), (32, True), (64, False)])
+def test_hmc_random_register_window_vs_oracle_and_windowed(gpu_lib, side, wall, monkeypatch):
+    """One star on a 32/48/64-px image takes the register-window kernel
+    (hmc_random_k1_tiledr): trajectories against the oracle and the windowed
+    kernel (RHMC_KERNEL=windowed) to 1e-10, identical stale-momentum flags,
+    ragged batch (the last wave partly empty, lengths differing inside a wave)."""
+    from oracle import rhmc_ref as R
+    capi = gpu_lib
+    setup = R.default_setup()
+    rs = np.random.RandomState(side + wall)
+    c = side / 2.0
+    f_true = R.mag2flux(19.) * setup["flux_to_count"]
+    D = rs.poisson(R.model_image(side, side, [(f_true, c + 0.2, c - 0.3)],
+                                 setup["B_count"], setup["fwhm_pix"])).astype(np.float64)
+    f_lim = 0.97 * f_true if wall else setup["B_count"]
+    par = dict(rows=side, cols=side, B_count=setup["B_count"], fwhm_pix=setup["fwhm_pix"],
+               use_prior=0, use_Vc=0, alpha=2., beta=1., Vc_r_pow=1., dt=1., f_lim=f_lim,
+               f_low=1., g_xx=1., g_ff=1., g_ff2=1., g0=1., g1=1., g2=1., fmin=-1., fmax=-1.)
+    m = R.RefModel(D, par)
+    P = capi.make_params(dt=1., delta=1e-6, counter_max=1000, B_count=par["B_count"],
+                         f_lim=f_lim, f_low=1., fwhm_pix=par["fwhm_pix"], g_xx=1., g_ff=1.,
+                         g_ff2=1., g0=1., g1=1., g2=1., use_prior=False, alpha=2.,
+                         use_Vc=False, beta=1., Vc_r_pow=1., V_prior_const=0.)
+    n = 203
+    q0 = np.stack([f_true * np.exp(0.1 * rs.randn(n)), c + 0.5 * rs.randn(n),
+                   c + 0.5 * rs.randn(n)], 1)
+    p0 = rs.randn(n, 3)
+    dt = np.array([2.0, 0.02, 0.02])
+    steps = rs.randint(1, 30, size=n).astype(np.int32)
+    ctx = capi.Context(D)
+    try:
+        q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
+        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        qw, pw, stw = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
+        monkeypatch.delenv("RHMC_KERNEL")
+        qs, ps = ctx.hmc_random(P, dt, q0[5:18], p0[5:18], steps[5:18])
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(qs, q[5:18])
+    np.testing.assert_array_equal(ps, p[5:18])
+    np.testing.assert_array_equal(st & capi.STATUS_REFLECT_F, stw & capi.STATUS_REFLECT_F)
+    for a, b in ((q, qw), (p, pw)):
+        assert (np.abs(a - b) / (np.abs(b) + 1)).max() <= 1e-10
+    stale = 0
+    for k in range(0, n, 10):
+        qo, po, flip = m.hmc_random_traj(q0[k], p0[k], dt, int(steps[k]), f_lim)
+        assert bool(st[k] & capi.STATUS_REFLECT_F) == flip, k
+        stale += flip
+        assert np.abs(q[k] - qo).max() / (np.abs(qo).max() + 1) <= 1e-10, k
+        assert np.abs(p[k] - po).max() / (np.abs(po).max() + 1) <= 1e-10, k
+    if wall:
+        assert (st & capi.STATUS_REFLECT_F).any()
