@@ -1349,6 +1349,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.side = ctx->rows;
     t.pad = 0;
     t.c = a.c;
+    t.dtv = nullptr;
+    t.steps = nullptr;
     return launch_kr(ctx, t, 0, s);
   }
   a.g = make_geometry(ctx->rows, ctx->cols);
@@ -1588,6 +1590,8 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
     t.side = ctx->rows;
     t.pad = 0;
     t.c = a.c;
+    t.dtv = nullptr;
+    t.steps = nullptr;
     HIP_TRY(hipSetDevice(ctx->device));
     const int fp = f_pos != 0;
     if (solver == RHMC_SOLVER_HMC) return launch_kr<RHMC_SOLVER_HMC>(ctx, t, fp, s);
@@ -1673,6 +1677,26 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
       case 48: return launch_hmc_random_k1<48>(ctx, t, d_dt, d_steps, s);
       default: return launch_hmc_random_k1<64>(ctx, t, d_dt, d_steps, s);
     }
+  }
+  // many stars: the multi-star register-window kernel (rhmc_tiledrk.hpp)
+  if (use_tiledrk(ctx, K, a.c) && !std::getenv("RHMC_KERNEL")) {
+    LeapArgsKR t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = nullptr;
+    t.status = d_st;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n;
+    t.K = K;
+    t.n_steps = 0;
+    t.side = ctx->rows;
+    t.pad = 0;
+    t.c = a.c;
+    t.dtv = d_dt;
+    t.steps = d_steps;
+    HIP_TRY(hipSetDevice(ctx->device));
+    return launch_kr<kSolverHmcRandom>(ctx, t, 0, s);
   }
   if (!window_exact(a.c)) return window_unsupported();  // windowed gradient
   a.q = d_q;

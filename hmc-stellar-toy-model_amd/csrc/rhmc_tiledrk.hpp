@@ -50,7 +50,13 @@ struct LeapArgsKR {
   int64_t n_chains;
   int K, n_steps, side, pad;
   Consts c;
+  const double* dtv;      // kSolverHmcRandom: per-coordinate steps [3K]
+  const int32_t* steps;   // kSolverHmcRandom: trajectory length per chain
 };
+
+// leapfrog_kr's SOLVER for samplers.HMC_random trajectories (not a C-ABI
+// solver: rhmc_hmc_random selects it).
+constexpr int kSolverHmcRandom = 100;
 
 struct KRStar {  // LDS star table entry
   double f, x, y, pad;
@@ -577,6 +583,85 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
   }
 }
 
+// samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552) for the
+// chain's stars: unit mass, per-coordinate steps dtv, n leapfrog steps, the
+// flux wall at c.f_lim with the reference's quirks (hmc_random_win_kernel: a
+// star's flip flag is never cleared; the flip applies on every step where ANY
+// of the chain's stars is below the wall).  p holds the half-step momentum;
+// returns true when the last step flipped — the caller then keeps the
+// starting momentum (:547-550).  dVdq without the metric (:365-425).
+template <int SLOTS, class GRAD>
+__device__ __forceinline__ bool km_hmc_random_steps(double (&f)[SLOTS], double (&x)[SLOTS],
+                                                    double (&y)[SLOTS], double (&pf)[SLOTS],
+                                                    double (&px)[SLOTS], double (&py)[SLOTS],
+                                                    const bool (&own)[SLOTS], KRStar* tab,
+                                                    int n, const double* __restrict__ dtv,
+                                                    const Consts& c, GRAD grad) {
+  const int m = lane_id() & 31;
+  // the steps are re-read from memory (L1/L2) where used instead of being held
+  // in registers across the gradient (register pressure at two slots)
+  // (the index goes through an empty asm so that the loads are not hoisted)
+  auto dti = [&](int t, int j) {
+    int i = 3 * (own[t] ? 32 * t + m : 0) + j;
+    asm volatile("" : "+v"(i));
+    return dtv[i];
+  };
+  auto dtf = [&](int t) { return dti(t, 0); };
+  auto dtx = [&](int t) { return dti(t, 1); };
+  auto dty = [&](int t) { return dti(t, 2); };
+  bool iflip[SLOTS];
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) iflip[t] = false;
+  double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+  auto gradient = [&]() {
+    grad(x, y, gf, gx, gy);
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t)
+      if (c.use_prior) gf[t] += c.alpha / f[t];    // :408-409
+  };
+  kr_publish<SLOTS>(tab, f, x, y, own);
+  gradient();
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {                // :519
+    pf[t] = pf[t] - dtf(t) * gf[t] / 2.0;
+    px[t] = px[t] - dtx(t) * gx[t] / 2.0;
+    py[t] = py[t] - dty(t) * gy[t] / 2.0;
+  }
+  bool flip = false;
+  for (int s = 0; s < n; ++s) {
+    bool below_any = false;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      f[t] = f[t] + dtf(t) * pf[t];                // :523
+      x[t] = x[t] + dtx(t) * px[t];
+      y[t] = y[t] + dty(t) * py[t];
+      const bool below = own[t] && f[t] < c.f_lim; // :526-529
+      iflip[t] = iflip[t] || below;
+      below_any = below_any || below;
+    }
+    flip = half_any(below_any);
+    kr_publish<SLOTS>(tab, f, x, y, own);
+    gradient();
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      const double kept = -pf[t];                  // :531
+      pf[t] = pf[t] - dtf(t) * gf[t];              // :532, :535
+      px[t] = px[t] - dtx(t) * gx[t];
+      py[t] = py[t] - dty(t) * gy[t];
+      if (flip && iflip[t]) pf[t] = kept;          // :533
+    }
+  }
+  if (!flip) {
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {              // :551-552
+      pf[t] = pf[t] + dtf(t) * gf[t] / 2.0;
+      px[t] = px[t] + dtx(t) * gx[t] / 2.0;
+      py[t] = py[t] + dty(t) * gy[t] / 2.0;
+    }
+  }
+  return flip;
+}
+
 // Two chains per wave (32 lanes each), W waves per workgroup; two waves per
 // SIMD (<= 256 VGPRs) except the fp64-image / K > 32 variant, which needs more.
 // SOLVER: RHMC_SOLVER_IMPLICIT = RHMC_single_step (km_steps), else one of the
@@ -606,7 +691,8 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   const int h = lane / TK::LPC, m = lane % TK::LPC;
   const int64_t chain = TK::CPW * wave + h;
   const bool real = chain < a.n_chains;  // ragged tail: mirror the wave's first chain
-  const int64_t cbase = (real ? chain : TK::CPW * wave) * 3 * (int64_t)a.K;
+  const int64_t chain_r = real ? chain : TK::CPW * wave;
+  const int64_t cbase = chain_r * 3 * (int64_t)a.K;
   const int W = blockDim.x / kWave;
   const int slot = (threadIdx.x / kWave) * TK::CPW + h;  // chain slot in the workgroup
   KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * TK::KMAX;
@@ -637,12 +723,25 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
                   double (&gx)[SLOTS], double (&gy)[SLOTS]) {
     TK::gradient(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy);
   };
-  if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT)
+  if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT) {
     km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc, grad,
                     it_p, it_q, st);
-  else
+  } else if constexpr (SOLVER == kSolverHmcRandom) {
+    if (km_hmc_random_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.steps[chain_r], a.dtv, c,
+                                   grad)) {
+      st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const int64_t e = cbase + 3 * (int64_t)(own[t] ? TK::LPC * t + m : 0);
+        pf[t] = own[t] ? a.p[e] : 0.0;
+        px[t] = own[t] ? a.p[e + 1] : 0.0;
+        py[t] = own[t] ? a.p[e + 2] : 0.0;
+      }
+    }
+  } else {
     km_explicit_steps<SOLVER, SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, f_pos, c, lc,
                                      grad, st);
+  }
 
   unsigned nf = 0u;
 #pragma unroll

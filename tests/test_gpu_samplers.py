@@ -168,3 +168,51 @@ def test_hmc_random_register_window_vs_oracle_and_windowed(gpu_lib, side, wall, 
         assert np.abs(p[k] - po).max() / (np.abs(po).max() + 1) <= 1e-10, k
     if wall:
         assert (st & capi.STATUS_REFLECT_F).any()
+
+
+@pytest.mark.parametrize("side,K,n", [(48, 10, 517), (48, 20, 37), (64, 40, 9)])
+def test_hmc_random_many_stars_vs_oracle_and_windowed(gpu_lib, side, K, n, monkeypatch):
+    """K >= 2 takes the multi-star register-window kernel (leapfrog_kr with
+    kSolverHmcRandom): trajectories against the windowed kernel and the oracle
+    to 1e-10, the flux wall hit by the faint stars (any star below flips every
+    star whose flag is set), identical stale-momentum flags, ragged batches."""
+    from oracle import rhmc_ref as R
+    from test_gpu_integrators import _star_field
+    capi = gpu_lib
+    wl = _star_field(side, K, n, 5 + K)
+    rs = np.random.RandomState(K)
+    fl = np.sort(wl.q0[0, 0::3])
+    f_lim = 0.9 * fl[2]                              # the faintest stars reach it
+    par = dict(rows=side, cols=side, B_count=wl.params["B_count"],
+               fwhm_pix=wl.params["fwhm_pix"], use_prior=0, use_Vc=0, alpha=2., beta=1.,
+               Vc_r_pow=1., dt=1., f_lim=f_lim, f_low=1., g_xx=1., g_ff=1., g_ff2=1., g0=1.,
+               g1=1., g2=1., fmin=-1., fmax=-1.)
+    m = R.RefModel(wl.D, par)
+    P = capi.make_params(dt=1., delta=1e-6, counter_max=1000, B_count=par["B_count"],
+                         f_lim=f_lim, f_low=1., fwhm_pix=par["fwhm_pix"], g_xx=1., g_ff=1.,
+                         g_ff2=1., g0=1., g1=1., g2=1., use_prior=False, alpha=2.,
+                         use_Vc=False, beta=1., Vc_r_pow=1., V_prior_const=0.)
+    q0 = wl.q0
+    p0 = rs.randn(*q0.shape)
+    dt = np.tile([1.0, 0.005, 0.005], K)
+    steps = rs.randint(1, 20, size=n).astype(np.int32)
+    ctx = capi.Context(wl.D)
+    try:
+        q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
+        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        qw, pw, stw = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
+        monkeypatch.delenv("RHMC_KERNEL")
+        idx = np.arange(min(n, 7))
+        qs, ps = ctx.hmc_random(P, dt, q0[idx], p0[idx], steps[idx])
+    finally:
+        ctx.close()
+    np.testing.assert_array_equal(qs, q[idx])
+    np.testing.assert_array_equal(ps, p[idx])
+    np.testing.assert_array_equal(st & capi.STATUS_REFLECT_F, stw & capi.STATUS_REFLECT_F)
+    for a, b in ((q, qw), (p, pw)):
+        assert (np.abs(a - b) / (np.abs(b) + 1)).max() <= 1e-10
+    for k in sorted({0, 1, n // 2, n - 1}):
+        qo, po, flip = m.hmc_random_traj(q0[k], p0[k], dt, int(steps[k]), f_lim)
+        assert bool(st[k] & capi.STATUS_REFLECT_F) == flip, k
+        assert np.abs(q[k] - qo).max() / (np.abs(qo).max() + 1) <= 1e-10, k
+        assert np.abs(p[k] - po).max() / (np.abs(po).max() + 1) <= 1e-10, k
