@@ -36,6 +36,7 @@
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
 #include "rhmc_mhk1.hpp"
+#include "rhmc_pixk.hpp"
 #include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -1266,6 +1267,32 @@ int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, int f_pos, hipStream_t s) {
              : launch_kr_t<double, 2, false, SOLVER>(ctx, a, f_pos, s);
 }
 
+// Pixel-major multi-star kernel (rhmc_pixk.hpp): the default for 2 <= K <= 10
+// on a 32/48-px fp32-exact image (C3: 1.23e8 chain-steps/s against 1.05e8 for
+// the window-major kernel with LDS tables, measured A/B on one box).  Any other
+// RHMC_KERNEL value keeps the older kernels.
+bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
+  const char* e = std::getenv("RHMC_KERNEL");
+  const bool want = !e || std::strcmp(e, "pixk") == 0;
+  return want && K >= 2 && K <= 10 && !c.use_Vc && ctx->img_f32 && ctx->rows == ctx->cols &&
+         (ctx->rows == 32 || ctx->rows == 48);
+}
+
+template <int IMG>
+int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
+  using PK = PixK<IMG, 10>;
+  int W = 4;
+  while (W > 1 && PK::lds_bytes(W) > (size_t)ctx->max_lds / 2) W >>= 1;
+  const size_t lds = PK::lds_bytes(W);
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "pixk LDS");
+  a.Df = ctx->d_Df;
+  const int64_t waves = (a.n_chains + PK::CPW - 1) / PK::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((leapfrog_pk<IMG, 10>), grid, block, lds, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s) {
@@ -1335,7 +1362,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
       default: return launch_tiled<64>(ctx, t, s);
     }
   }
-  if (use_tiledrk(ctx, K, a.c)) {
+  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -1351,6 +1378,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.c = a.c;
     t.dtv = nullptr;
     t.steps = nullptr;
+    if (use_pixk(ctx, K, a.c)) return ctx->rows == 32 ? launch_pk<32>(ctx, t, s) : launch_pk<48>(ctx, t, s);
     return launch_kr(ctx, t, 0, s);
   }
   a.g = make_geometry(ctx->rows, ctx->cols);

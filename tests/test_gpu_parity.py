@@ -21,7 +21,7 @@ def _ctx(capi, z):
     return capi.Context(z["D"])
 
 
-@pytest.fixture(params=["auto", "generic", "windowed", "tiledk", "tiledrk", "tiledrk_notab", "tiled1", "tiled2", "tiledw", "tiledw32", "tiledr64", "tiledl1", "tiledl4", "tiledl1_64"])
+@pytest.fixture(params=["auto", "generic", "windowed", "tiledk", "tiledrk", "tiledrk_notab", "pixk", "tiled1", "tiled2", "tiledw", "tiledw32", "tiledr64", "tiledl1", "tiledl4", "tiledl1_64"])
 def kernel_path(request, monkeypatch):
     """Run a test on the automatically chosen kernel, then again forced onto
     the generic LDS-image kernel and onto the windowed large-image kernel."""
