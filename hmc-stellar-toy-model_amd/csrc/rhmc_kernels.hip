@@ -1278,8 +1278,8 @@ bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
          (ctx->rows == 32 || ctx->rows == 48);
 }
 
-template <int IMG>
-int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
+template <int IMG, int SOLVER = RHMC_SOLVER_IMPLICIT>
+int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s, int f_pos = 0) {
   using PK = PixK<IMG, 10>;
   int W = 4;
   while (W > 1 && PK::lds_bytes(W) > (size_t)ctx->max_lds / 2) W >>= 1;
@@ -1288,9 +1288,15 @@ int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s) {
   a.Df = ctx->d_Df;
   const int64_t waves = (a.n_chains + PK::CPW - 1) / PK::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_pk<IMG, 10>), grid, block, lds, s, a);
+  hipLaunchKernelGGL((leapfrog_pk<IMG, 10, SOLVER>), grid, block, lds, s, a, f_pos);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
+}
+
+template <int SOLVER>
+int launch_pk_side(const rhmc_ctx* ctx, const LeapArgsKR& a, hipStream_t s, int f_pos) {
+  return ctx->rows == 32 ? launch_pk<32, SOLVER>(ctx, a, s, f_pos)
+                         : launch_pk<48, SOLVER>(ctx, a, s, f_pos);
 }
 
 int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
@@ -1622,6 +1628,12 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
     t.steps = nullptr;
     HIP_TRY(hipSetDevice(ctx->device));
     const int fp = f_pos != 0;
+    if (use_pixk(ctx, K, a.c)) {
+      if (solver == RHMC_SOLVER_HMC) return launch_pk_side<RHMC_SOLVER_HMC>(ctx, t, s, fp);
+      if (solver == RHMC_SOLVER_RHMC_NAIVE)
+        return launch_pk_side<RHMC_SOLVER_RHMC_NAIVE>(ctx, t, s, fp);
+      return launch_pk_side<RHMC_SOLVER_RHMC_LEAPFROG>(ctx, t, s, fp);
+    }
     if (solver == RHMC_SOLVER_HMC) return launch_kr<RHMC_SOLVER_HMC>(ctx, t, fp, s);
     if (solver == RHMC_SOLVER_RHMC_NAIVE) return launch_kr<RHMC_SOLVER_RHMC_NAIVE>(ctx, t, fp, s);
     return launch_kr<RHMC_SOLVER_RHMC_LEAPFROG>(ctx, t, fp, s);
@@ -1724,6 +1736,7 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
     t.dtv = d_dt;
     t.steps = d_steps;
     HIP_TRY(hipSetDevice(ctx->device));
+    if (use_pixk(ctx, K, a.c)) return launch_pk_side<kSolverHmcRandom>(ctx, t, s, 0);
     return launch_kr<kSolverHmcRandom>(ctx, t, 0, s);
   }
   if (!window_exact(a.c)) return window_unsupported();  // windowed gradient

@@ -123,9 +123,11 @@ struct PixK {
 };
 
 // Two chains per wave, W waves per workgroup, one star per lane (K <= KMAX).
-template <int IMG, int KMAX>
+// SOLVER as in leapfrog_kr: RHMC_single_step, an explicit integrator (f_pos =
+// the flux wall) or kSolverHmcRandom.
+template <int IMG, int KMAX, int SOLVER = RHMC_SOLVER_IMPLICIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
-leapfrog_pk(LeapArgsKR a) {
+leapfrog_pk(LeapArgsKR a, int f_pos) {
   using PK = PixK<IMG, KMAX>;
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;
@@ -160,12 +162,25 @@ leapfrog_pk(LeapArgsKR a) {
   py[0] = own[0] ? a.p[e + 2] : 0.0;
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  km_steps<1>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(IMG - 1), c, lc,
-              [&](const double (&)[1], const double (&)[1], double (&gf)[1], double (&gx)[1],
+  auto grad = [&](const double (&)[1], const double (&)[1], double (&gf)[1], double (&gx)[1],
                   double (&gy)[1]) {
-                PK::gradient(lds, simg, tab, rtab, K, c, lc, gf[0], gx[0], gy[0]);
-              },
-              it_p, it_q, st);
+    PK::gradient(lds, simg, tab, rtab, K, c, lc, gf[0], gx[0], gy[0]);
+  };
+  if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT) {
+    km_steps<1>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(IMG - 1), c, lc, grad, it_p,
+                it_q, st);
+  } else if constexpr (SOLVER == kSolverHmcRandom) {
+    if (km_hmc_random_steps<1>(f, x, y, pf, px, py, own, tab, a.steps[chain_r], a.dtv, c,
+                               grad)) {
+      st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
+      pf[0] = own[0] ? a.p[e] : 0.0;
+      px[0] = own[0] ? a.p[e + 1] : 0.0;
+      py[0] = own[0] ? a.p[e + 2] : 0.0;
+    }
+  } else {
+    km_explicit_steps<SOLVER, 1>(f, x, y, pf, px, py, own, tab, a.n_steps, f_pos, c, lc, grad,
+                                 st);
+  }
   unsigned nf = 0u;
   if (own[0] && real) {
     if (!(isfinite(f[0]) && isfinite(x[0]) && isfinite(y[0]) && isfinite(pf[0]) &&

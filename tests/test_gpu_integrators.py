@@ -159,6 +159,7 @@ def _star_field(side, K, n_chains, seed):
 
 @pytest.mark.parametrize("name", SOLVERS)
 @pytest.mark.parametrize("side,K,n_chains", [(48, 10, 16384),   # C3: LDS factor tables
+                                             (32, 4, 301),      # pixel-major, 32-px image
                                              (48, 20, 37),      # exp path, one star slot
                                              (64, 40, 5)])      # two star slots per lane
 def test_many_star_explicit_vs_oracle(gpu_lib, name, side, K, n_chains, monkeypatch):

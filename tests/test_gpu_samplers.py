@@ -170,7 +170,7 @@ def test_hmc_random_register_window_vs_oracle_and_windowed(gpu_lib, side, wall, 
         assert (st & capi.STATUS_REFLECT_F).any()
 
 
-@pytest.mark.parametrize("side,K,n", [(48, 10, 517), (48, 20, 37), (64, 40, 9)])
+@pytest.mark.parametrize("side,K,n", [(48, 10, 517), (32, 4, 129), (48, 20, 37), (64, 40, 9)])
 def test_hmc_random_many_stars_vs_oracle_and_windowed(gpu_lib, side, K, n, monkeypatch):
     """K >= 2 takes the multi-star register-window kernel (leapfrog_kr with
     kSolverHmcRandom): trajectories against the windowed kernel and the oracle
