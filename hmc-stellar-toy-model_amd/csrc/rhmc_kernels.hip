@@ -1609,8 +1609,9 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
       default: return launch_integrate_tiledr<64>(ctx, t, solver, fp, s);
     }
   }
-  // many stars: the multi-star register-window kernel (rhmc_tiledrk.hpp)
-  if (use_tiledrk(ctx, K, a.c)) {
+  // many stars: the pixel-major kernel (full image, any PSF width) or the
+  // multi-star register-window kernel (rhmc_tiledrk.hpp, 28-px windows)
+  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -1718,8 +1719,12 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
       default: return launch_hmc_random_k1<64>(ctx, t, d_dt, d_steps, s);
     }
   }
-  // many stars: the multi-star register-window kernel (rhmc_tiledrk.hpp)
-  if (use_tiledrk(ctx, K, a.c) && !std::getenv("RHMC_KERNEL")) {
+  // many stars: the pixel-major kernel (full image, any PSF width) or the
+  // multi-star register-window kernel (rhmc_tiledrk.hpp); RHMC_KERNEL=tiledrk
+  // forces the latter, any other override keeps the windowed kernel below.
+  const char* ke = std::getenv("RHMC_KERNEL");
+  const bool kr = use_tiledrk(ctx, K, a.c) && (!ke || std::strncmp(ke, "tiledrk", 7) == 0);
+  if (use_pixk(ctx, K, a.c) || kr) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;

@@ -222,9 +222,11 @@ struct TiledR {
     return group_sum(v);
   }
 
-  // The row slice's sums of the chain's dphidq pixel terms: s0 = sum psf s,
-  // s1 = sum psf s dx, s2 = sum psf s dy (s = D/Lambda - 1; every lane of the
-  // chain gets them).
+  // The row slice's sums of the chain's dphidq pixel terms, all three scaled
+  // by the flux: s0 = f sum psf s, s1 = f sum psf s dx, s2 = f sum psf s dy
+  // (s = D/Lambda - 1; every lane of the chain gets them).  The column
+  // factors carry f (fey = f ey serves Lambda and both sums), so no separate
+  // f ex row factors are held: 14 VGPRs and 7 products fewer.
   static __device__ __forceinline__ void partial(const double* __restrict__ etab,
                                                  const DT* __restrict__ sD, Cache& k, double f,
                                                  double x, double y, const Consts& c,
@@ -241,11 +243,11 @@ struct TiledR {
     // pixels (row-major): 1/(l0 l1 l2 l3) by v_rcp_f64 + one Newton step, then
     // 1/l0 = l1 l2 l3 r etc. by products (v_rcp_f64 issues at a quarter of the
     // FMA rate); then the separable row / column sums (rhmc_tiled2.hpp).
-    double R[TR], C[TC], fe[TR];
+    double R[TR], C[TC];
 #pragma unroll
-    for (int i = 0; i < TR; ++i) fe[i] = f * ex[i];
+    for (int j = 0; j < TC; ++j) ey[j] = f * ey[j];
     auto lam = [&](int pp) {  // Lambda at pixel pp (:373-376)
-      return fma(fe[pp / TC], ey[pp % TC], c.B);
+      return fma(ex[pp / TC], ey[pp % TC], c.B);
     };
     auto acc = [&](int pp, double sv) {  // row / column sums of s (D/Lambda - 1, :379)
       const int i = pp / TC, j = pp % TC;
@@ -287,28 +289,25 @@ struct TiledR {
       constexpr int pp = NPX - 1;
       acc(pp, fma((double)k.d[pp], rcpn(lam(pp)), -1.0));
     }
-    double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0;
+    // a0 = sum_i ex_i R_i is also sum_j fey_j C_j: it serves both moments
+    double a0 = 0.0, a1 = 0.0, w1 = 0.0;
 #pragma unroll
     for (int i = 0; i < TR; ++i) {
       const double tt = ex[i] * R[i];
       a0 += tt;
-      a1 = fma(tt, (double)i, a1);
+      if (i > 0) a1 = fma(tt, (double)i, a1);
     }
 #pragma unroll
-    for (int j = 0; j < TC; ++j) {
-      const double w = ey[j] * C[j];
-      w0 += w;
-      w1 = fma(w, (double)(4 * j), w1);
-    }
+    for (int j = 1; j < TC; ++j) w1 = fma(ey[j] * C[j], (double)(4 * j), w1);
     const double dxa = ((r0 + (double)(ROW0 + TR * a)) - x) + 0.5;  // lane's row 0 offset
     const double dyb = ((c0 + (double)b) - y) + 0.5;                // lane's column 0 offset
     s0 = group_sum(a0);
     s1 = group_sum(fma(dxa, a0, a1));
-    s2 = group_sum(fma(dyb, w0, w1));
+    s2 = group_sum(fma(dyb, a0, w1));
   }
 
   // Pixel part of the chain's dphidq over the slice (the whole window for the
-  // default slice).
+  // default slice).  partial's sums carry f: gx, gy need no f, gf one 1/f.
   static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
                                                   const DT* __restrict__ sD, Cache& k,
                                                   double f, double x, double y, const Consts& c,
@@ -316,9 +315,9 @@ struct TiledR {
                                                   double& gy) {
     double s0, s1, s2;
     partial(etab, sD, k, f, x, y, c, lc, s0, s1, s2);
-    gf = -s0;                                          // :404
-    gx = -s1 * f * lc.inv_var;                         // :405
-    gy = -s2 * f * lc.inv_var;                         // :406
+    gf = -s0 * rcp_nr1(f);                             // :404
+    gx = -s1 * lc.inv_var;                             // :405
+    gy = -s2 * lc.inv_var;                             // :406
   }
 };
 

@@ -467,31 +467,31 @@ class multi_gym(base_class):
                     self.A_chain[l] = 1
                 else:
                     q_tmp = self.q_chain[l, :self.d]
-                continue
-            # reversible-jump moves (:1089-1187): Nsteps RHMC steps, momentum
-            # flip, the dimension-changing proposal, Nsteps steps, flip, then
-            # accept with ln alpha0 = -dE + factor
-            grow = np.random.choice([True, False], p=[0.5, 0.5])
-            self.move_chain[l] = (1 if grow else 2) if move_type == 1 else (3 if grow else 4)
-            q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
-                                           counter_max=counter_max)
-            p_tmp = -p_tmp
-            move = self.birth_death_move if move_type == 1 else self.split_merge_move
-            q_tmp, p_tmp, factor = move(q_tmp, p_tmp, grow)
-            q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
-                                           counter_max=counter_max)
-            p_tmp = -p_tmp
-            H_diag = self.H(q_tmp, grad=False)
-            E_final = self.V(q_tmp, f_pos=f_pos) + self.T(p_tmp, H_diag)
-            ln_alpha0 = -(E_final - E_initial) + factor
-            lnu = np.log(np.random.random(1))
-            if (ln_alpha0 > 0) or (lnu < ln_alpha0):
-                self.A_chain[l] = 1
-            else:                                         # undo the dimension change
-                self.Nobjs += -1 if grow else 1
-                self.d = 3 * self.Nobjs
-                q_tmp = self.q_chain[l, :self.d]
-            if verbose and (l % 50) == 0:
+            else:
+                # reversible-jump moves (:1089-1187): Nsteps RHMC steps, momentum
+                # flip, the dimension-changing proposal, Nsteps steps, flip, then
+                # accept with ln alpha0 = -dE + factor
+                grow = np.random.choice([True, False], p=[0.5, 0.5])
+                self.move_chain[l] = (1 if grow else 2) if move_type == 1 else (3 if grow else 4)
+                q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
+                                               counter_max=counter_max)
+                p_tmp = -p_tmp
+                move = self.birth_death_move if move_type == 1 else self.split_merge_move
+                q_tmp, p_tmp, factor = move(q_tmp, p_tmp, grow)
+                q_tmp, p_tmp = self.RHMC_steps(q_tmp, p_tmp, self.Nsteps, delta=delta,
+                                               counter_max=counter_max)
+                p_tmp = -p_tmp
+                H_diag = self.H(q_tmp, grad=False)
+                E_final = self.V(q_tmp, f_pos=f_pos) + self.T(p_tmp, H_diag)
+                ln_alpha0 = -(E_final - E_initial) + factor
+                lnu = np.log(np.random.random(1))
+                if (ln_alpha0 > 0) or (lnu < ln_alpha0):
+                    self.A_chain[l] = 1
+                else:                                         # undo the dimension change
+                    self.Nobjs += -1 if grow else 1
+                    self.d = 3 * self.Nobjs
+                    q_tmp = self.q_chain[l, :self.d]
+            if verbose and (l % 50) == 0:                 # :1183-1186, every move type
                 print("/---- Completed iteration %d" % l)
                 print("N_objs: %d\n" % self.Nobjs)
                 self.R_accept_report(idx_iter=l, run_window=10)

@@ -101,3 +101,21 @@ def test_datagen_numpy_path_matches_reference(name, cls):
     np.testing.assert_array_equal(g.centers_noise, z[name + "/centers"])
     with pytest.raises(ValueError):
         g.gen_mock_data(stars, rng="bogus")
+
+
+def test_run_RHMC_verbose_report_after_move0(capsys):
+    """The verbose progress block (sampler_RHMC.py:1183-1186) runs after every
+    move type, including the fixed-dimension move 0: N_objs and the running
+    acceptance report are printed at l % 50 == 0.  The device-backed step and
+    energy are stubbed (host control flow only)."""
+    from rhmc_amd import sampler
+    g = sampler.multi_gym(g_xx=1., g_ff=1., g_ff2=1.)
+    g.fmin, g.fmax = 1.0, 1e4
+    g.RHMC_steps = lambda q, p, n, delta=1e-6, counter_max=1000: (q, p)
+    g.V = lambda q, f_pos=True: 0.0
+    np.random.seed(0)
+    g.run_RHMC(np.array([[19., 24.3, 23.8]]), Niter=50, Nsteps=3, verbose=True)
+    out = capsys.readouterr().out
+    assert "Completed iteration 0" in out and "Completed iteration 50" in out
+    assert out.count("N_objs: 1") == 2
+    assert g.A_chain.all()                        # dE = T1 - T0 = 0 with the stubs
