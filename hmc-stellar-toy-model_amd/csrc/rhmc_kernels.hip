@@ -1280,7 +1280,7 @@ bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
 
 template <int IMG, int SOLVER = RHMC_SOLVER_IMPLICIT>
 int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s, int f_pos = 0) {
-  using PK = PixK<IMG, 10>;
+  using PK = PixK<IMG, 10>;  // LDS layout does not depend on the columns per pass
   int W = 4;
   while (W > 1 && PK::lds_bytes(W) > (size_t)ctx->max_lds / 2) W >>= 1;
   const size_t lds = PK::lds_bytes(W);

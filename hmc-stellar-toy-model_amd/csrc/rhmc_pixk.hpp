@@ -3,34 +3,133 @@
 // of the image and the window-major kernel (rhmc_tiledrk.hpp) evaluates Lambda
 // about 3.9 times per pixel.  Here Lambda is evaluated once per image pixel,
 // as the reference does (sampler_RHMC.py:373-376, full image), and the three
-// per-star sums of dphidq (:404-406) come out of separable accumulations:
-//   s0_k = sum_j ey_k(j) sum_i ex_k(i) s_ij
-//   s1_k = sum_j ey_k(j) sum_i (i + 1/2 - x_k) ex_k(i) s_ij
-//   s2_k = sum_j (j + 1/2 - y_k) ey_k(j) sum_i ex_k(i) s_ij,  s = D/Lambda - 1.
+// per-star sums of dphidq (:404-406) come out of separable accumulations with
+// offsets taken from the image centre ctr = IMG/2 (w_i = i + 1/2 - ctr):
+//   c0_k(j) = sum_i ex_k(i) s_ij,   c1_k(j) = sum_i ex_k(i) w_i s_ij
+//   A0_k = sum_j fey_k(j) c0_k(j)   (= f_k sum PSF_k s)
+//   A1_k = sum_j fey_k(j) c1_k(j),  A2_k = sum_j w_j fey_k(j) c0_k(j)
+// and sum PSF_k s (i + 1/2 - x_k) f_k = A1_k + (ctr - x_k) A0_k, likewise y:
+// so the row table holds ex only and the column factors carry f (fey), which
+// serves Lambda and all three sums.  s = D/Lambda - 1.
 // 32 lanes per chain (two chains per wave64): lane m = 16 rh + cg owns image
-// columns cg, cg + 16, ... and rows rh IMG/2 .. rh IMG/2 + IMG/2 - 1.  Row
-// factors ex_k(i), (i + 1/2 - x_k) ex_k(i) sit in a per-chain LDS table
-// [IMG][KMAX][2] (rebuilt per gradient, read by 16 lanes at a time); the
-// column factors of the lane's current column are in registers (f ey for
-// Lambda, ey for the sums).  The step loop is km_steps (rhmc_tiledrk.hpp).
+// columns cg, cg + 16, ... and rows rh IMG/2 .. rh IMG/2 + IMG/2 - 1.  Per
+// gradient each chain builds two LDS tables, ex_k(i) [IMG][KMAX] and
+// fey_k(j) [IMG][KMAX] (2 IMG KMAX / 32 exps per lane); a lane then runs its
+// columns CT at a time: fey of its CT columns in registers, each row's ex
+// read once (KMAX/2 ds_read_b128, broadcast to the 16 lanes of a row half)
+// and used for CT pixels, whose data values sit side by side in the LDS image
+// (layout [row][cg][NCP]: one ds_read_b64 per row for a column pair) and
+// share one v_rcp_f64.  The step loop is km_steps (rhmc_tiledrk.hpp).
 #pragma once
 #include "rhmc_tiledrk.hpp"
 
 namespace rhmc {
 
-template <int IMG, int KMAX>
+// Image columns per pass of the pixel-major gradient (1 to 3; capped at the
+// lane's column count).
+#ifndef RHMC_PK_CT
+#define RHMC_PK_CT 3
+#endif
+
+template <int IMG, int KMAX, int CT_ = RHMC_PK_CT>
 struct PixK {
   static constexpr int LPC = 32;           // lanes per chain
   static constexpr int CPW = kWave / LPC;  // chains per wave
   static constexpr int NC = IMG / 16;      // columns per lane
+  static constexpr int NCP = (NC + 1) & ~1;  // LDS image: values per (row, column group)
   static constexpr int NR = IMG / 2;       // rows per lane
-  static_assert(IMG % 32 == 0 || IMG == 48, "image side");
-  static constexpr size_t row_tab_doubles() { return (size_t)IMG * KMAX * 2; }
-  // LDS: exp table, star tables (32 per chain), row tables, image (fp32 [IMG][IMG]).
+  static constexpr int CT = CT_ < NC ? CT_ : NC;
+  static constexpr double kCtr = IMG / 2;
+  static_assert(IMG == 32 || IMG == 48, "image side");
+  static_assert(CT >= 1 && CT <= 3, "columns per pass");
+  // per chain: row table ex [IMG][KMAX], then column table fey [IMG][KMAX]
+  static constexpr size_t tab_doubles() { return (size_t)2 * IMG * KMAX; }
+  // LDS: exp table, star tables (32 per chain), factor tables, image (fp32
+  // [IMG][16][NCP]).
   static __host__ __device__ constexpr size_t lds_bytes(int waves) {
     return kExpTab * sizeof(double) + (size_t)waves * CPW * LPC * sizeof(KRStar) +
-           (size_t)waves * CPW * row_tab_doubles() * sizeof(double) +
-           (size_t)IMG * IMG * sizeof(float);
+           (size_t)waves * CPW * tab_doubles() * sizeof(double) +
+           (size_t)IMG * 16 * NCP * sizeof(float);
+  }
+  // LDS image index of pixel (r, col)
+  static __device__ __forceinline__ int img_index(int r, int col) {
+    return (r * 16 + (col & 15)) * NCP + (col >> 4);
+  }
+
+  // Columns ci0 .. ci0 + N - 1 of the lane: accumulate their per-star sums
+  // into A0, A1, A2.
+  template <int N>
+  static __device__ __forceinline__ void columns(int ci0, const float* __restrict__ simg,
+                                                 const double* rtab, const double* ctab, int K,
+                                                 const Consts& c, double (&A0)[KMAX],
+                                                 double (&A1)[KMAX], double (&A2)[KMAX]) {
+    const int m = lane_id() & (LPC - 1);
+    const int cg = m & 15, rh = m >> 4;
+    double fey[N][KMAX], c0[N][KMAX], c1[N][KMAX];
+#pragma unroll
+    for (int q = 0; q < N; ++q)
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        fey[q][k] = ctab[(cg + 16 * (ci0 + q)) * KMAX + k];
+        c0[q][k] = c1[q][k] = 0.0;
+      }
+    const double* rt = rtab + (size_t)(rh * NR) * KMAX;
+    const float* dp = simg + (rh * NR * 16 + cg) * NCP + ci0;
+// rows per loop iteration
+#ifndef RHMC_PK_ROW_UNROLL
+#define RHMC_PK_ROW_UNROLL 4
+#endif
+#pragma unroll RHMC_PK_ROW_UNROLL
+    for (int r = 0; r < NR; ++r) {
+      double ex[KMAX];
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) ex[k] = rt[r * KMAX + k];
+      double l[N], sv[N];
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        l[q] = c.B;  // Lambda, stars in ascending order (:373-376)
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) l[q] = fma(ex[k], fey[q][k], l[q]);
+      }
+      if constexpr (N == 3) {  // one reciprocal for the three pixels
+        const float4 d = *reinterpret_cast<const float4*>(dp + r * 16 * NCP);
+        const double l01 = l[0] * l[1];
+        const double rr = rcp_nr1(l01 * l[2]);
+        const double r01 = l[2] * rr;
+        sv[0] = fma((double)d.x, l[1] * r01, -1.0);  // D/Lambda - 1 (:379)
+        sv[1] = fma((double)d.y, l[0] * r01, -1.0);
+        sv[2] = fma((double)d.z, l01 * rr, -1.0);
+      } else if constexpr (N == 2) {  // one reciprocal for the pixel pair
+        const float2 d = *reinterpret_cast<const float2*>(dp + r * 16 * NCP);
+        const double rr = rcp_nr1(l[0] * l[1]);
+        sv[0] = fma((double)d.x, l[1] * rr, -1.0);  // D/Lambda - 1 (:379)
+        sv[1] = fma((double)d.y, l[0] * rr, -1.0);
+      } else {
+        sv[0] = fma((double)dp[r * 16 * NCP], rcp_nr1(l[0]), -1.0);
+      }
+      const double w = ((double)(rh * NR + r) + 0.5) - kCtr;
+#pragma unroll
+      for (int q = 0; q < N; ++q) {
+        const double t = w * sv[q];
+#pragma unroll
+        for (int k = 0; k < KMAX; ++k) {
+          c0[q][k] = fma(ex[k], sv[q], c0[q][k]);
+          c1[q][k] = fma(ex[k], t, c1[q][k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < N; ++q) {
+      const double wj = ((double)(cg + 16 * (ci0 + q)) + 0.5) - kCtr;
+#pragma unroll
+      for (int k = 0; k < KMAX; ++k) {
+        if (k < K) {  // wave-uniform
+          A0[k] = fma(fey[q][k], c0[q][k], A0[k]);
+          A1[k] = fma(fey[q][k], c1[q][k], A1[k]);
+          A2[k] = fma(wj * fey[q][k], c0[q][k], A2[k]);
+        }
+      }
+    }
   }
 
   // Pixel part of dphidq (:365-425 without metric / prior): lane m < K gets
@@ -41,69 +140,29 @@ struct PixK {
                                                   const Consts& c, const LeanConsts& lc,
                                                   double& gf, double& gx, double& gy) {
     const int m = lane_id() & (LPC - 1);
-    const int cg = m & 15, rh = m >> 4;
+    double* ctab = rtab + (size_t)IMG * KMAX;
     wave_lds_sync();  // the previous gradient's table reads are done
     for (int e = m; e < IMG * KMAX; e += LPC) {
       const int i = e / KMAX, k = e - (e / KMAX) * KMAX;
-      double ex = 0.0, dex = 0.0;
+      double ex = 0.0, fey = 0.0;
       if (k < K) {
         const double v = ((double)i + 0.5) - tab[k].x;
         ex = exp_neg(-(v * v) * lc.inv_two_sig2, etab);
-        dex = v * ex;
+        const double u = ((double)i + 0.5) - tab[k].y;
+        fey = tab[k].f * (exp_neg(-(u * u) * lc.inv_two_sig2, etab) * lc.inv_norm);
       }
-      rtab[2 * e] = ex;
-      rtab[2 * e + 1] = dex;
+      rtab[e] = ex;
+      ctab[e] = fey;
     }
     wave_lds_sync();
     double A0[KMAX], A1[KMAX], A2[KMAX];
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) A0[k] = A1[k] = A2[k] = 0.0;
-#pragma unroll 1
-    for (int ci = 0; ci < NC; ++ci) {
-      const int j = cg + 16 * ci;
-      // column factors: f ey for Lambda here, ey again at the column's end
-      // (recomputed rather than held: registers)
-      auto col_factor = [&](int k) {
-        const double v = ((double)j + 0.5) - tab[k].y;
-        return exp_neg(-(v * v) * lc.inv_two_sig2, etab) * lc.inv_norm;
-      };
-      double fey[KMAX], c0[KMAX], c1[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        fey[k] = c0[k] = c1[k] = 0.0;
-        if (k < K) fey[k] = tab[k].f * col_factor(k);  // wave-uniform guard
-      }
-      const double* rt = rtab + (size_t)(rh * NR) * KMAX * 2;
-      const float* dc = simg + (rh * NR) * IMG + j;
-// rows per loop iteration (measured at C3: 1 -> 4 +2 %, 8 equal to 4, a full
-// unroll of the 24 rows 22x slower)
-#ifndef RHMC_PK_ROW_UNROLL
-#define RHMC_PK_ROW_UNROLL 4
-#endif
-#pragma unroll RHMC_PK_ROW_UNROLL
-      for (int r = 0; r < NR; ++r) {
-        const double* t0 = rt + (size_t)r * KMAX * 2;
-        double l0 = c.B;  // Lambda, stars in ascending order (:373-376)
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) l0 = fma(t0[2 * k], fey[k], l0);
-        const double s0 = fma((double)dc[r * IMG], rcp_nr1(l0), -1.0);  // D/Lambda - 1 (:379)
-#pragma unroll
-        for (int k = 0; k < KMAX; ++k) {
-          c0[k] = fma(t0[2 * k], s0, c0[k]);
-          c1[k] = fma(t0[2 * k + 1], s0, c1[k]);
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < KMAX; ++k) {
-        if (k < K) {  // wave-uniform
-          const double ey = col_factor(k);
-          const double dy = ((double)j + 0.5) - tab[k].y;
-          A0[k] = fma(ey, c0[k], A0[k]);
-          A1[k] = fma(ey, c1[k], A1[k]);
-          A2[k] = fma(dy * ey, c0[k], A2[k]);
-        }
-      }
-    }
+    for (int ci = 0; ci + CT <= NC; ci += CT)
+      columns<CT>(ci, simg, rtab, ctab, K, c, A0, A1, A2);
+    if constexpr (NC % CT == 1) columns<1>(NC - 1, simg, rtab, ctab, K, c, A0, A1, A2);
+    static_assert(NC % CT <= 1, "column passes");
     gf = gx = gy = 0.0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -112,10 +171,10 @@ struct PixK {
         const double s1 = half_sum_dpp(A1[k]);
         const double s2 = half_sum_dpp(A2[k]);
         if (m == k) {
-          const double fk = tab[k].f;
-          gf = -s0;                      // :404
-          gx = -s1 * fk * lc.inv_var;    // :405
-          gy = -s2 * fk * lc.inv_var;    // :406
+          const KRStar st = tab[k];
+          gf = -s0 / st.f;                                  // :404
+          gx = -fma(kCtr - st.x, s0, s1) * lc.inv_var;      // :405
+          gy = -fma(kCtr - st.y, s0, s2) * lc.inv_var;      // :406
         }
       }
     }
@@ -128,13 +187,16 @@ struct PixK {
 template <int IMG, int KMAX, int SOLVER = RHMC_SOLVER_IMPLICIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_pk(LeapArgsKR a, int f_pos) {
-  using PK = PixK<IMG, KMAX>;
+  // HMC_random keeps a little more state across the gradient: two columns
+  // per pass there (three spill)
+  using PK = PixK<IMG, KMAX, (SOLVER == kSolverHmcRandom ? 2 : RHMC_PK_CT)>;
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;
   exp_tab_fill(lds);
   float* simg = reinterpret_cast<float*>(lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
-                                         (size_t)W * PK::CPW * PK::row_tab_doubles());
-  for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) simg[e] = a.Df[e];
+                                         (size_t)W * PK::CPW * PK::tab_doubles());
+  for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x)
+    simg[PK::img_index(e / IMG, e % IMG)] = a.Df[e];
   __syncthreads();
   const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (PK::CPW * wave >= a.n_chains) return;
@@ -146,7 +208,7 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   const int64_t cbase = chain_r * 3 * (int64_t)a.K;
   const int slot = (threadIdx.x / kWave) * PK::CPW + h;
   KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * PK::LPC;
-  double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 + (size_t)slot * PK::row_tab_doubles();
+  double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 + (size_t)slot * PK::tab_doubles();
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
   const int K = a.K;
@@ -167,19 +229,19 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
     PK::gradient(lds, simg, tab, rtab, K, c, lc, gf[0], gx[0], gy[0]);
   };
   if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT) {
-    km_steps<1>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(IMG - 1), c, lc, grad, it_p,
-                it_q, st);
+    km_steps<1, decltype(grad), true>(f, x, y, pf, px, py, own, tab, a.n_steps,
+                                      (double)(IMG - 1), c, lc, grad, it_p, it_q, st);
   } else if constexpr (SOLVER == kSolverHmcRandom) {
-    if (km_hmc_random_steps<1>(f, x, y, pf, px, py, own, tab, a.steps[chain_r], a.dtv, c,
-                               grad)) {
+    if (km_hmc_random_steps<1, decltype(grad), true>(f, x, y, pf, px, py, own, tab,
+                                                     a.steps[chain_r], a.dtv, c, grad)) {
       st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
       pf[0] = own[0] ? a.p[e] : 0.0;
       px[0] = own[0] ? a.p[e + 1] : 0.0;
       py[0] = own[0] ? a.p[e + 2] : 0.0;
     }
   } else {
-    km_explicit_steps<SOLVER, 1>(f, x, y, pf, px, py, own, tab, a.n_steps, f_pos, c, lc, grad,
-                                 st);
+    km_explicit_steps<SOLVER, 1, decltype(grad), true>(f, x, y, pf, px, py, own, tab,
+                                                       a.n_steps, f_pos, c, lc, grad, st);
   }
   unsigned nf = 0u;
   if (own[0] && real) {

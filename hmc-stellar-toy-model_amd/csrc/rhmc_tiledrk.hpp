@@ -341,11 +341,28 @@ __device__ __forceinline__ void kr_publish(KRStar* tab, const double (&f)[SLOTS]
   wave_lds_sync();
 }
 
+// The chain's (f, x, y) back from its star table (RELOAD step loops: the
+// state is not held in registers across a gradient that reads it from the
+// table anyway; lanes without a star get the placeholder 1, 0, 0).
+template <int SLOTS>
+__device__ __forceinline__ void kr_reload(const KRStar* tab, double (&f)[SLOTS],
+                                          double (&x)[SLOTS], double (&y)[SLOTS],
+                                          const bool (&own)[SLOTS]) {
+  const int m = lane_id() & 31;
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    const KRStar e = tab[own[t] ? 32 * t + m : 0];
+    f[t] = own[t] ? e.f : 1.0;
+    x[t] = own[t] ? e.x : 0.0;
+    y[t] = own[t] ? e.y : 0.0;
+  }
+}
+
 // n_steps steps of RHMC_single_step (sampler_RHMC.py:522-566) for the chain's
 // stars (lane m: stars m + 32 t).  The end-of-step gradient is carried into
 // the next step; the flux metric is computed once per distinct f
 // (rhmc_k1step.hpp); the loops stop on np.max(|dq|) <= delta, NaN included.
-template <int SLOTS, class GRAD>
+template <int SLOTS, class GRAD, bool RELOAD = false>
 __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
                                          double (&y)[SLOTS], double (&pf)[SLOTS],
                                          double (&px)[SLOTS], double (&py)[SLOTS],
@@ -360,6 +377,7 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
   for (int s = 0;; ++s) {
     double gf[SLOTS], gx[SLOTS], gy[SLOTS];
     grad(x, y, gf, gx, gy);
+    if constexpr (RELOAD) kr_reload<SLOTS>(tab, f, x, y, own);
     // Recompute the flux metric instead of keeping it live through the
     // gradient (register pressure): the asm hides f's value from CSE.
 #pragma unroll
@@ -480,7 +498,7 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
 // lean FluxMetric; p/H is p A (flux) and p s/g_xx (positions).  The gradient
 // and metric at the end of a step are the next step's first ones; the metric
 // is recomputed after each gradient rather than held across it (km_steps).
-template <int SOLVER, int SLOTS, class GRAD>
+template <int SOLVER, int SLOTS, class GRAD, bool RELOAD = false>
 __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x)[SLOTS],
                                                   double (&y)[SLOTS], double (&pf)[SLOTS],
                                                   double (&px)[SLOTS], double (&py)[SLOTS],
@@ -501,6 +519,7 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
   };
   auto gradient = [&]() {  // dVdq (:365-425) at the published state
     grad(x, y, gf, gx, gy);
+    if constexpr (RELOAD) kr_reload<SLOTS>(tab, f, x, y, own);
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t)
       if (c.use_prior) gf[t] += c.alpha / f[t];     // :408-409
@@ -590,7 +609,7 @@ __device__ __forceinline__ void km_explicit_steps(double (&f)[SLOTS], double (&x
 // of the chain's stars is below the wall).  p holds the half-step momentum;
 // returns true when the last step flipped — the caller then keeps the
 // starting momentum (:547-550).  dVdq without the metric (:365-425).
-template <int SLOTS, class GRAD>
+template <int SLOTS, class GRAD, bool RELOAD = false>
 __device__ __forceinline__ bool km_hmc_random_steps(double (&f)[SLOTS], double (&x)[SLOTS],
                                                     double (&y)[SLOTS], double (&pf)[SLOTS],
                                                     double (&px)[SLOTS], double (&py)[SLOTS],
@@ -615,6 +634,7 @@ __device__ __forceinline__ bool km_hmc_random_steps(double (&f)[SLOTS], double (
   double gf[SLOTS], gx[SLOTS], gy[SLOTS];
   auto gradient = [&]() {
     grad(x, y, gf, gx, gy);
+    if constexpr (RELOAD) kr_reload<SLOTS>(tab, f, x, y, own);
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t)
       if (c.use_prior) gf[t] += c.alpha / f[t];    // :408-409
