@@ -62,11 +62,88 @@ __device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
   return m;
 }
 
+// Lane-parallel q-loop passes (QL = 16 lanes per chain, one DPP row).
+#ifndef RHMC_QPAR
+#define RHMC_QPAR 1
+#endif
+constexpr bool kQPar = RHMC_QPAR;
+
+__device__ __forceinline__ double row_shr1(double v) {  // lane l of a 16-lane row gets lane l - 1
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, 0x111, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), 0x111, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// The q-loop (:538-545) with the chain's 16 lanes evaluating 8 iterations at
+// once.  The flux iterates are an affine recurrence F' = bf F + cf, so lane j
+// (j = lane % 8; lanes j and j + 8 duplicate) gets F_j = T^j(F_0) by binary
+// powering of T (three conditional FMAs; rounding differs from the sequential
+// chain by a few ulp, like the affine form itself), then F_{j+1} = T(F_j) and
+// the position iterates X_{j+1}, Y_{j+1} = b g(F_j) + c; X_j, Y_j come from
+// lane j - 1 by a DPP row shift.  The reference's test for iteration j
+// (np.max |q_j - q_{j+1}| > delta, NaN stops, counter_max) is evaluated in lane
+// j; a ballot gives the first stopping iteration k of each chain, whose state
+// q_{k+1} is read from lane k (ds_bpermute).  A chain with no stop among the 8
+// takes q_8 and runs another pass.  Same iterates, counts and cap status as
+// the sequential loop; one rcp chain per 8 iterations instead of per iteration.
+__device__ __forceinline__ void q_loop_lanes16(double& f, double& x, double& y, double bf,
+                                               double cf, double bx, double cx, double by,
+                                               double cy, const Consts& c, const LeanConsts& lc,
+                                               int& it_q, unsigned& st) {
+  const int lane = lane_id();
+  const int j = lane & 7;
+  const int gsh = lane & 48;  // first lane of the chain's row
+  // T^2, T^4 (wave-uniform per chain)
+  const double b2 = bf * bf, c2 = fma(bf, cf, cf);
+  const double b4 = b2 * b2, c4 = fma(b2, c2, c2);
+  int n = 0;
+  bool done = false, more = false;
+  do {
+    double Fj = f;
+    if (j & 1) Fj = fma(bf, Fj, cf);
+    if (j & 2) Fj = fma(b2, Fj, c2);
+    if (j & 4) Fj = fma(b4, Fj, c4);
+    const double Fj1 = fma(bf, Fj, cf);
+    const double fl = (Fj < lc.f_low) ? lc.f_low : Fj;
+    const double u = rcp_nr1(fl);
+    const double g = u * fma(lc.Bg2, u, lc.inv_g1);
+    const double Xj1 = fma(bx, g, cx), Yj1 = fma(by, g, cy);
+    double Xj = row_shr1(Xj1), Yj = row_shr1(Yj1);
+    if (j == 0) {
+      Xj = x;
+      Yj = y;
+    }
+    const double a0 = fabs(Fj - Fj1), a1 = fabs(Xj - Xj1), a2 = fabs(Yj - Yj1);
+    const double sum = a0 + a1 + a2;
+    const bool go = (fmax(fmax(a0, a1), a2) > c.delta) && (sum == sum);
+    const bool stop = !go || (n + j + 1 >= c.counter_max);
+    const unsigned long long bal = __builtin_amdgcn_ballot_w64(stop);
+    const unsigned bits = (unsigned)(bal >> gsh) & 0xFFu;
+    const int k = bits ? (int)__builtin_ctz(bits) : 7;
+    const int src = gsh + k;
+    const double nf = __shfl(Fj1, src, kWave), nx = __shfl(Xj1, src, kWave),
+                 ny = __shfl(Yj1, src, kWave);
+    const int ngo = __shfl((int)go, src, kWave);
+    if (!done) {
+      f = nf;
+      x = nx;
+      y = ny;
+      n += k + 1;
+      more = ngo != 0;
+      done = bits != 0u;
+    }
+  } while (__builtin_amdgcn_ballot_w64(!done) != 0);
+  it_q += n;
+  if (more) st |= RHMC_STATUS_QLOOP_CAP;
+}
+
 // n_steps steps on (f, x, y, pf, px, py).  grad(f, x, y, gf, gx, gy) returns
 // the pixel part of dphidq: gf = -sum psf (D/L - 1), gx, gy (:404-406).
 // PROF (tools only): per-phase cycle sums, prof[0] gradient, prof[1] kicks +
 // reflection + p-loop, prof[2] q-loop, prof[3] flux metric + closing update.
-template <bool PROF = false, class GRAD>
+// QL: lanes per chain (16: the q-loop runs 8 iterations per pass across them).
+template <bool PROF = false, int QL = 1, class GRAD>
 __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double& pf,
                                          double& px, double& py, int n_steps, double edge,
                                          const Consts& c, const LeanConsts& lc, GRAD grad,
@@ -162,6 +239,9 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       const double bf = hdt * (pf * lc.inv_gff2), cf = f + hdt * (pf * fm.A + pf * lc.c0);
       const double bx = hdt * (px * lc.inv_gxx), cx = x + hdt * (px * ihxx_s);
       const double by = hdt * (py * lc.inv_gxx), cy = y + hdt * (py * ihxx_s);
+      if constexpr (QL == 16 && kQPar) {
+        q_loop_lanes16(f, x, y, bf, cf, bx, cx, by, cy, c, lc, it_q, st);
+      } else {
       bool more;
       int n = 0;
       do {
@@ -205,6 +285,7 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       } while (more && n < c.counter_max);
       it_q += n;
       if (more) st |= RHMC_STATUS_QLOOP_CAP;
+      }
       RHMC_MARK(4);
     }
     mark(2);

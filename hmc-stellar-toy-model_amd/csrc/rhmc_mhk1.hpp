@@ -172,7 +172,7 @@ mh_k1_tiledr(MhK1Args a) {
     y1 = y;
     int it_p = 0, it_q = 0;
     unsigned st = 0u;
-    k1_steps(f1, x1, y1, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
+    k1_steps<false, TL::LPC>(f1, x1, y1, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
              [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
                TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
              },

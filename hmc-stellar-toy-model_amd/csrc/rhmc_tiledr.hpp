@@ -355,7 +355,7 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
   long long prof[4] = {0, 0, 0, 0};
-  k1_steps<PROF>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
+  k1_steps<PROF, TL::LPC>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
                  [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
                    TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
                  },
