@@ -62,6 +62,11 @@ __device__ __forceinline__ double swizzle_d(double v) {
 #endif
 constexpr int kRcpGroup = RHMC_RCP_GROUP;
 
+// PSF factors by recurrence (factors_rec; 0: four exps per lane, factors).
+#ifndef RHMC_FACT_REC
+#define RHMC_FACT_REC 1
+#endif
+
 // DT: the type the window pixels are cached in (float when the image is
 // exactly representable in fp32, else double).
 //
@@ -195,6 +200,62 @@ struct TiledR {
     }
   }
 
+  // The same factors (ey times `scale`) from ONE exp per lane and two
+  // multiplicative recurrences.  With v = r0 + i + 1/2 - x and c = 1/(2 sigma^2),
+  //   ex(v + 1) = ex(v) g(v),  g(v) = exp(-c (2 v + 1)),  g(v + 1) = g(v) e^{-2c};
+  // with w = c0 + j + 1/2 - y,
+  //   ey(w + 4) = ey(w) h(w),  h(w) = exp(-c (8 w + 16)), h(w + 4) = h(w) e^{-32c}.
+  // Lane (a, b) evaluates b = 0: ex at row group a's first row, b = 1: its g,
+  // b = 2: ey at column a, b = 3: its h; DPP quad broadcasts hand the row
+  // values round the quad, ds_bpermute the column values (lane (b, 2), (b, 3)).
+  // Each factor is at most TR - 1 products from an exp: within ~25 ulp of the
+  // direct exp (the direct factors already differ from the reference's
+  // exp(-(dx^2 + dy^2) c) by a few ulp).  A wave with a chain so far from its
+  // window that a base exp or a ratio could leave the fp64 range
+  // (|v0| or |w0| >= rec_vmax, or NaN) takes the direct factors instead.
+  static __device__ __forceinline__ void factors_rec(const double* __restrict__ etab,
+                                                     const Cache& k, double x, double y,
+                                                     const LeanConsts& lc, double scale,
+                                                     double (&ex)[TR], double (&ey)[TC]) {
+#if RHMC_FACT_REC
+    const int lane = lane_id();
+    const int m = lane % LPC;
+    const int a = m / 4, b = m % 4;
+    const double c = lc.inv_two_sig2;
+    const double v0 = (k.r0 + ((double)(ROW0 + TR * a) + 0.5)) - x;  // row group a, first row
+    const double w0 = (k.c0 + ((double)a + 0.5)) - y;                // column a
+    const bool ok = fabs(v0) < lc.rec_vmax && fabs(w0) < lc.rec_vmax;
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+      const double z = (b < 2) ? v0 : w0;
+      const double lin = (b < 2) ? fma(2.0, z, 1.0) : fma(8.0, z, 16.0);
+      const double t = ((b & 1) ? lin : z * z) * -c;
+      const double e = exp_neg(t, etab);
+      const double ex0 = row_bcast<0>(e), g0 = row_bcast<1>(e);
+      const int src = (lane & ~(LPC - 1)) + 4 * b;
+      const double ey0 = __shfl(e, src + 2, kWave) * (lc.inv_norm * scale);
+      const double h0 = __shfl(e, src + 3, kWave);
+      ex[0] = ex0;
+      double g = g0;
+#pragma unroll
+      for (int i = 1; i < TR; ++i) {
+        ex[i] = ex[i - 1] * g;
+        if (i + 1 < TR) g = g * lc.k_row;
+      }
+      ey[0] = ey0;
+      double h = h0;
+#pragma unroll
+      for (int j = 1; j < TC; ++j) {
+        ey[j] = ey[j - 1] * h;
+        if (j + 1 < TC) h = h * lc.k_col4;
+      }
+      return;
+    }
+#endif
+    factors(etab, k, x, y, lc, ex, ey);
+#pragma unroll
+    for (int j = 0; j < TC; ++j) ey[j] = scale * ey[j];
+  }
+
   // The window's part of the chain's potential V (sampler_RHMC.py:294-302,
   // Lambda :373-376) relative to the background-only image:
   //   sum_window (Lambda - B) - D (ln Lambda - ln B).
@@ -208,7 +269,7 @@ struct TiledR {
                                                             const LeanConsts& lc, double lnB) {
     ensure(sD, k, x, y);
     double ex[TR], ey[TC];
-    factors(etab, k, x, y, lc, ex, ey);
+    factors_rec(etab, k, x, y, lc, 1.0, ex, ey);
     double v = 0.0;
 #pragma unroll
     for (int i = 0; i < TR; ++i) {
@@ -237,15 +298,13 @@ struct TiledR {
     ensure(sD, k, x, y);
     const double r0 = k.r0, c0 = k.c0;
     double ex[TR], ey[TC];
-    factors(etab, k, x, y, lc, ex, ey);
+    factors_rec(etab, k, x, y, lc, f, ex, ey);  // ey carries f
 
     // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
     // pixels (row-major): 1/(l0 l1 l2 l3) by v_rcp_f64 + one Newton step, then
     // 1/l0 = l1 l2 l3 r etc. by products (v_rcp_f64 issues at a quarter of the
     // FMA rate); then the separable row / column sums (rhmc_tiled2.hpp).
     double R[TR], C[TC];
-#pragma unroll
-    for (int j = 0; j < TC; ++j) ey[j] = f * ey[j];
     auto lam = [&](int pp) {  // Lambda at pixel pp (:373-376)
       return fma(ex[pp / TC], ey[pp % TC], c.B);
     };

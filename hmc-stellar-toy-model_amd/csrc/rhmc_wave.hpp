@@ -24,6 +24,10 @@ struct Consts {
   // reciprocals for the division-lean forms, computed once on the host (a
   // device-side computation gets re-materialised inside the step loop)
   double inv_gff2, inv_g1, Bg2, inv_gxx, inv_two_sig2, inv_norm, inv_var;
+  // PSF factor recurrences (rhmc_tiledr.hpp factors): ratio of successive row
+  // ratios exp(-2/(2 sigma^2)), of column ratios 4 apart exp(-32/(2 sigma^2)),
+  // and the largest |window offset| for which the recurrence stays in range
+  double k_row, k_col4, rec_vmax;
   int counter_max, use_prior, use_Vc, pad;
 };
 
@@ -110,6 +114,7 @@ __device__ __forceinline__ double rcp_nr(double d) {  // ~correctly rounded 1/d
 struct LeanConsts {
   double inv_gff2, c0, inv_g1, Bg2, inv_gxx, f_low;
   double inv_two_sig2, inv_norm, inv_var;  // PSF exponent / normalisation, 1/var
+  double k_row, k_col4, rec_vmax;          // PSF factor recurrences (Consts)
 };
 
 __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
@@ -123,6 +128,9 @@ __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
   l.inv_two_sig2 = c.inv_two_sig2;
   l.inv_norm = c.inv_norm;
   l.inv_var = c.inv_var;
+  l.k_row = c.k_row;
+  l.k_col4 = c.k_col4;
+  l.rec_vmax = c.rec_vmax;
   return l;
 }
 
