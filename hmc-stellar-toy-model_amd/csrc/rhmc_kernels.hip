@@ -895,11 +895,12 @@ int make_consts(const rhmc_params* P, Consts* c) {
     c->k_row = std::exp(-2.0 * ci);
     c->k_col4 = std::exp(-32.0 * ci);
     // |v0| < rec_vmax keeps every base exp above the fp64 normal range
-    // (c v0^2 < 700) and every ratio within e^+-300 over 8 rows / 8 columns
-    // 4 apart: c (2 (|v0| + 8) + 1) < 300, c (8 (|v0| + 32) + 16) < 300
+    // (c v0^2 < 700) and every ratio below e^700 over up to 8 rows (row
+    // ratios: c (2 (|v0| + 8) + 1) < 700) or 8 columns 4 apart (column
+    // ratios: c (8 (|w0| + 32) + 16) < 700); outside it the direct factors run
     double vm = std::sqrt(700.0 / ci);
-    vm = std::fmin(vm, (300.0 / ci - 17.0) / 2.0);
-    vm = std::fmin(vm, 300.0 / (8.0 * ci) - 34.0);
+    vm = std::fmin(vm, (700.0 / ci - 17.0) / 2.0);
+    vm = std::fmin(vm, 700.0 / (8.0 * ci) - 34.0);
     c->rec_vmax = (ci > 0.0 && vm > 0.0) ? vm : 0.0;
   }
   c->counter_max = P->counter_max;

@@ -58,7 +58,7 @@ __device__ __forceinline__ double swizzle_d(double v) {
 
 // Pixels sharing one v_rcp_f64 in the pixel loop (2 or 4).
 #ifndef RHMC_RCP_GROUP
-#define RHMC_RCP_GROUP 2
+#define RHMC_RCP_GROUP 4
 #endif
 constexpr int kRcpGroup = RHMC_RCP_GROUP;
 
