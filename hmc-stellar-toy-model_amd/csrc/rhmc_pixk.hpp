@@ -30,6 +30,10 @@ namespace rhmc {
 #ifndef RHMC_PK_CT
 #define RHMC_PK_CT 3
 #endif
+// Factor tables by recurrence (PixK::tables_rec; 0: one exp per entry).
+#ifndef RHMC_PK_REC
+#define RHMC_PK_REC 1
+#endif
 
 template <int IMG, int KMAX, int CT_ = RHMC_PK_CT>
 struct PixK {
@@ -132,6 +136,68 @@ struct PixK {
     }
   }
 
+  // The factor tables by recurrence (utils.py:475-486 evaluated as in
+  // rhmc_tiledr.hpp factors_rec): lane m < S KMAX owns star k = m / S and the
+  // image rows (for ex) / columns (for fey) of segment m % S, SR = ceil(IMG / S)
+  // of them, in runs of up to 8 that start from two exps each,
+  //   e(v) = exp(-c v^2), g(v) = exp(-c (2 v + 1)), e(v + 1) = e(v) g(v),
+  //   g(v + 1) = g(v) e^{-2c}   (v = i + 1/2 - x_k),
+  // i.e. 8 exps per lane for both tables instead of 30 (C3).  Each entry is at
+  // most 7 products from an exp (within ~25 ulp of the direct exp).  Returns
+  // false (nothing written) when a run of some lane of the wave starts outside
+  // the recurrence's range (|v| >= rec_vmax, NaN): the caller then evaluates
+  // every entry directly.  Phantom stars (k >= K) get zeros.
+  static __device__ __forceinline__ bool tables_rec(const double* __restrict__ etab,
+                                                    const KRStar* tab, double* rtab,
+                                                    double* ctab, int K, const LeanConsts& lc) {
+    constexpr int S = LPC / KMAX;            // segments per star
+    constexpr int SR = (IMG + S - 1) / S;    // rows / columns per segment
+    constexpr int RUN = 8;                   // entries per exp pair
+    static_assert(S >= 1, "stars per chain");
+    // lane id by a volatile read: the loop-invariant segment bookkeeping below
+    // is recomputed per gradient instead of being hoisted out of the step loop
+    // (its registers would stay live across the pixel passes and spill)
+    int lid;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+    const int m = lid & (LPC - 1);
+    const bool act = m < S * KMAX;
+    const int k = act ? m / S : 0, seg = act ? m - (m / S) * S : 0;
+    const bool real = act && k < K;
+    const double c = lc.inv_two_sig2;
+    const KRStar st = tab[real ? k : 0];
+    const double xs = real ? st.x : 0.0, ys = real ? st.y : 0.0;
+    bool ok = true;
+#pragma unroll
+    for (int r0 = 0; r0 < SR; r0 += RUN) {
+      const double o = (double)(seg * SR + r0) + 0.5;
+      ok = ok && fabs(o - xs) < lc.rec_vmax && fabs(o - ys) < lc.rec_vmax;
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
+    if (!act) return true;
+    const double fn = real ? st.f * lc.inv_norm : 0.0;
+#pragma unroll 1
+    for (int t = 0; t < 2; ++t) {  // t = 0: row table ex, t = 1: column table fey
+      const double ctr = t ? ys : xs;
+      double* dst = (t ? ctab : rtab) + k;
+#pragma unroll 1
+      for (int r0 = 0; r0 < SR; r0 += RUN) {
+        const int ib = seg * SR + r0;
+        const double v0 = ((double)ib + 0.5) - ctr;
+        double e = exp_neg(-(v0 * v0) * c, etab);
+        double g = exp_neg(-fma(2.0, v0, 1.0) * c, etab);
+        if (t) e = e * fn;  // f (e N): one rounding more than f * (e * N)
+        if (!real) e = 0.0;
+#pragma unroll
+        for (int l = 0; l < RUN && r0 + l < SR; ++l) {
+          if (ib + l < IMG) dst[(ib + l) * KMAX] = e;
+          e = e * g;
+          g = g * lc.k_row;
+        }
+      }
+    }
+    return true;
+  }
+
   // Pixel part of dphidq (:365-425 without metric / prior): lane m < K gets
   // star m's; the star table `tab` holds the chain's (f, x, y).
   static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
@@ -142,6 +208,9 @@ struct PixK {
     const int m = lane_id() & (LPC - 1);
     double* ctab = rtab + (size_t)IMG * KMAX;
     wave_lds_sync();  // the previous gradient's table reads are done
+#if RHMC_PK_REC
+    if (!tables_rec(etab, tab, rtab, ctab, K, lc))
+#endif
     for (int e = m; e < IMG * KMAX; e += LPC) {
       const int i = e / KMAX, k = e - (e / KMAX) * KMAX;
       double ex = 0.0, fey = 0.0;
