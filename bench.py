@@ -17,6 +17,9 @@ Extra objects on the JSON line:
                 profiles/*.json (rocprofv3 PMC), or null.
   cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on the host cores, one
                 chain per process, bounded sample (rank 0, N=1 only).
+  end_to_end    (leapfrog mode) the host-buffer C-ABI call rhmc_leapfrog on the
+                same chains: H2D + fused launch + D2H, synchronous — the
+                PCIe-inclusive rate a NumPy caller sees; never `value`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2]
        (N>1: launched by torch.distributed.run, one rank per GPU)
@@ -170,6 +173,8 @@ def main():
                     help="total chains split over the ranks (strong scaling, e.g. C4 = 2^20)")
     ap.add_argument("--leap", type=int, default=None, help="leapfrog steps per launch")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="skip the host-buffer (rhmc_leapfrog, PCIe-inclusive) measurement")
     ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "hmc_random", "datagen"),
                     default="leapfrog",
                     help="mh: whole MH iterations on device (momentum draw, V+T, accept; "
@@ -360,12 +365,31 @@ def main():
         "valu_active_frac": pmc.get("valu_active_frac"),
         "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
     }
+    if args.mode == "leapfrog" and not args.no_e2e:
+        out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)
     if rank == 0:
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def end_to_end(ctx, P, q, p, wl, leap, reps=3):
+    """The host-buffer boundary (rhmc_leapfrog): caller-owned
+    host q/p in, H2D + the fused launch + D2H, synchronous — what the drop-in
+    RHMC_single_step replacement costs a NumPy caller.  Reported beside
+    `value` (never as it); after the timed region, from the current states."""
+    qh, ph = q.cpu().numpy(), p.cpu().numpy()
+    ctx.leapfrog(P, qh, ph, leap, K=wl.K)           # warm (allocations, copies)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        qh, ph = ctx.leapfrog(P, qh, ph, leap, K=wl.K)
+    wall = (time.perf_counter() - t0) / reps
+    return {"value": wl.n_chains * leap / wall, "unit": "chain-leapfrog-steps/s",
+            "ms_per_call": wall * 1e3, "calls": reps,
+            "what": "rhmc_leapfrog on host arrays: H2D q/p, %d fused steps, D2H, sync "
+                    "(includes the numpy copies of the Python shim)" % leap}
 
 
 if __name__ == "__main__":

@@ -268,13 +268,24 @@ struct TiledRK {
           R[i] = (j == 0) ? ey[j] * sv : fma(ey[j], sv, R[i]);
           C[j] = (i == 0) ? ex[i] * sv : fma(ex[i], sv, C[j]);
         };
+        static_assert(NPX % 4 == 0, "pixel groups of four");
 #pragma unroll
-        for (int pp = 0; pp < NPX; pp += 2) {
-          const double l0 = lam[pp], l1 = lam[pp + 1];
-          const double L = l0 * l1;
-          const double r = rcp_nr1(L);
-          acc(pp, fma((double)d[pp], l1 * r, -1.0));
-          acc(pp + 1, fma((double)d[pp + 1], l0 * r, -1.0));
+        for (int pp = 0; pp < NPX; pp += kRcpGroup) {
+          if constexpr (kRcpGroup == 4) {  // one v_rcp_f64 per 4 pixels (rhmc_tiledr.hpp)
+            const double l0 = lam[pp], l1 = lam[pp + 1], l2 = lam[pp + 2], l3 = lam[pp + 3];
+            const double l01 = l0 * l1, l23 = l2 * l3;
+            const double r = rcp_nr1(l01 * l23);
+            const double r01 = l23 * r, r23 = l01 * r;
+            acc(pp, fma((double)d[pp], l1 * r01, -1.0));
+            acc(pp + 1, fma((double)d[pp + 1], l0 * r01, -1.0));
+            acc(pp + 2, fma((double)d[pp + 2], l3 * r23, -1.0));
+            acc(pp + 3, fma((double)d[pp + 3], l2 * r23, -1.0));
+          } else {
+            const double l0 = lam[pp], l1 = lam[pp + 1];
+            const double r = rcp_nr1(l0 * l1);
+            acc(pp, fma((double)d[pp], l1 * r, -1.0));
+            acc(pp + 1, fma((double)d[pp + 1], l0 * r, -1.0));
+          }
         }
         double a0 = 0.0, a1 = 0.0, w0 = 0.0, w1 = 0.0;
 #pragma unroll

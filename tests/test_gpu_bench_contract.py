@@ -1,0 +1,39 @@
+"""bench.py's JSON line (the driver's contract): one short run of the default
+C2 workload in a child process, checked for the fields the driver and the
+judge read — metric/value/unit, the roofline object, the host-buffer
+end_to_end rate beside (not as) value."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.gpu
+def test_bench_json_line():
+    out = subprocess.run([sys.executable, "bench.py", "--no-cpu", "--steps", "2", "--warmup", "1"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["metric"].startswith("chain-leapfrog-steps/sec, 48x48 1-star 4096 chains")
+    assert d["unit"] == "chain-leapfrog-steps/s" and d["higher_is_better"] is True
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1
+    assert d["dtype"] == "f64" and d["scaling"] == "weak"
+    assert d["config"]["chains_per_gpu"] == 4096 and d["config"]["K"] == 1
+    assert d["config"]["leapfrog_steps_per_launch"] == 500
+    assert d["value"] > 1e8                       # the north star's 1e8 target
+    r = d["roofline"]
+    for key in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms"):
+        assert key in r
+    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+    # value counts wall time around the launches, kernel_ms the launches alone
+    assert d["ms_per_step"] >= 0.9 * r["kernel_ms"]
+    assert d["nonfinite_chains"] == 0
+    e = d["end_to_end"]
+    assert e["unit"] == d["unit"] and 0 < e["value"] <= 1.05 * d["value"]
+    assert d["cpu_baseline"] is None              # --no-cpu
