@@ -213,10 +213,13 @@ struct TiledR {
   // exp(-(dx^2 + dy^2) c) by a few ulp).  A wave with a chain so far from its
   // window that a base exp or a ratio could leave the fp64 range
   // (|v0| or |w0| >= rec_vmax, or NaN) takes the direct factors instead.
+  static __device__ __forceinline__ void no_mark(int) {}
+  template <bool PROFG = false, class MARK = void (*)(int)>
   static __device__ __forceinline__ void factors_rec(const double* __restrict__ etab,
                                                      const Cache& k, double x, double y,
                                                      const LeanConsts& lc, double scale,
-                                                     double (&ex)[TR], double (&ey)[TC]) {
+                                                     double (&ex)[TR], double (&ey)[TC],
+                                                     MARK gmark = no_mark) {
 #if RHMC_FACT_REC
     const int lane = lane_id();
     const int m = lane % LPC;
@@ -230,6 +233,10 @@ struct TiledR {
       const double lin = (b < 2) ? fma(2.0, z, 1.0) : fma(8.0, z, 16.0);
       const double t = ((b & 1) ? lin : z * z) * -c;
       const double e = exp_neg(t, etab);
+      if constexpr (PROFG) {
+        asm volatile("" ::"v"(e));
+        gmark(4);
+      }
       const double ex0 = row_bcast<0>(e), g0 = row_bcast<1>(e);
       const int src = (lane & ~(LPC - 1)) + 4 * b;
       const double ey0 = __shfl(e, src + 2, kWave) * (lc.inv_norm * scale);
@@ -288,17 +295,34 @@ struct TiledR {
   // (s = D/Lambda - 1; every lane of the chain gets them).  The column
   // factors carry f (fey = f ey serves Lambda and both sums), so no separate
   // f ex row factors are held: 14 VGPRs and 7 products fewer.
+  // PROFG (tools only): fenced clock reads split the gradient into gp[3] window
+  // check, gp[4] range check + exp, gp[0] factor broadcasts + recurrences,
+  // gp[1] pixel loop, gp[2] moments + reductions.
+  template <bool PROFG = false>
   static __device__ __forceinline__ void partial(const double* __restrict__ etab,
                                                  const DT* __restrict__ sD, Cache& k, double f,
                                                  double x, double y, const Consts& c,
                                                  const LeanConsts& lc, double& s0, double& s1,
-                                                 double& s2) {
+                                                 double& s2, long long* gp = nullptr) {
+    long long t0 = 0;
+    auto gmark = [&](int bkt) {
+      if constexpr (PROFG) {
+        __builtin_amdgcn_sched_barrier(0);
+        const long long t1 = clock64();
+        if (bkt >= 0) gp[bkt] += t1 - t0;
+        t0 = t1;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    };
+    gmark(-1);
     const int m = lane_id() % LPC;
     const int a = m / 4, b = m % 4;
     ensure(sD, k, x, y);
+    gmark(3);
     const double r0 = k.r0, c0 = k.c0;
     double ex[TR], ey[TC];
-    factors_rec(etab, k, x, y, lc, f, ex, ey);  // ey carries f
+    factors_rec<PROFG>(etab, k, x, y, lc, f, ex, ey, gmark);  // ey carries f
+    gmark(0);
 
     // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
     // pixels (row-major): 1/(l0 l1 l2 l3) by v_rcp_f64 + one Newton step, then
@@ -348,6 +372,7 @@ struct TiledR {
       constexpr int pp = NPX - 1;
       acc(pp, fma((double)k.d[pp], rcpn(lam(pp)), -1.0));
     }
+    gmark(1);
     // a0 = sum_i ex_i R_i is also sum_j fey_j C_j: it serves both moments
     double a0 = 0.0, a1 = 0.0, w1 = 0.0;
 #pragma unroll
@@ -363,17 +388,22 @@ struct TiledR {
     s0 = group_sum(a0);
     s1 = group_sum(fma(dxa, a0, a1));
     s2 = group_sum(fma(dyb, a0, w1));
+    if constexpr (PROFG) {  // the sums must be complete at the mark
+      asm volatile("" ::"v"(s0), "v"(s1), "v"(s2));
+      gmark(2);
+    }
   }
 
   // Pixel part of the chain's dphidq over the slice (the whole window for the
   // default slice).  partial's sums carry f: gx, gy need no f, gf one 1/f.
+  template <bool PROFG = false>
   static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
                                                   const DT* __restrict__ sD, Cache& k,
                                                   double f, double x, double y, const Consts& c,
                                                   const LeanConsts& lc, double& gf, double& gx,
-                                                  double& gy) {
+                                                  double& gy, long long* gp = nullptr) {
     double s0, s1, s2;
-    partial(etab, sD, k, f, x, y, c, lc, s0, s1, s2);
+    partial<PROFG>(etab, sD, k, f, x, y, c, lc, s0, s1, s2, gp);
     gf = -s0 * rcp_nr1(f);                             // :404
     gx = -s1 * lc.inv_var;                             // :405
     gy = -s2 * lc.inv_var;                             // :406
@@ -413,10 +443,11 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
   TL::init(cache);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  long long prof[4] = {0, 0, 0, 0};
+  long long prof[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
   k1_steps<PROF, TL::LPC>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
                  [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
-                   TL::gradient(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy);
+                   TL::template gradient<PROF>(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy,
+                                               prof + 4);
                  },
                  it_p, it_q, st, prof);
   if constexpr (PROF) {  // tools only: cycles per step per phase replace the state
@@ -425,6 +456,11 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
     x = prof[1] / ns;
     y = prof[2] / ns;
     pf = prof[3] / ns;
+    px = prof[4] / ns;  // gradient: window check + factors
+    py = prof[5] / ns;  // pixel loop (prof[6], moments + reductions: it_p)
+    it_p = (int)(prof[6] / ns);
+    it_q = (int)(prof[7] / ns);  // window check
+    st = (unsigned)(prof[8] / ns);  // ok ballot + the exp
   }
 
   if ((lane % TL::LPC) == 0 && real) {

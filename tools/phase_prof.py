@@ -37,6 +37,11 @@ if kern.startswith("profr"):
     ph = [qq[:, 0].mean(), qq[:, 1].mean(), qq[:, 2].mean(), pp[:, 0].mean()]
     print("%s n=%d cycles/step: gradient %.0f  kicks+p-loop %.0f  q-loop %.0f  flux+tail %.0f"
           "  total %.0f" % (kern, n, ph[0], ph[1], ph[2], ph[3], sum(ph)))
+    itn = it.cpu().numpy().astype(float)
+    g5 = [itn[:, 1].mean(), st.cpu().numpy().astype(float).mean(), pp[:, 1].mean(),
+          pp[:, 2].mean(), itn[:, 0].mean()]
+    print("  gradient split: window check %.0f  range check + exp %.0f  broadcasts + "
+          "recurrences %.0f  pixel loop %.0f  moments + reductions %.0f" % tuple(g5))
 else:
     a = it.cpu().numpy().astype(float)
     print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
