@@ -34,6 +34,70 @@ namespace rhmc {
 #ifndef RHMC_PK_REC
 #define RHMC_PK_REC 1
 #endif
+// The 3 KMAX per-star sums by one 32-lane reduce-scatter (0: one all-reduce
+// per sum).
+#ifndef RHMC_PK_RS
+#define RHMC_PK_RS 1
+#endif
+
+// v with the double's halves through update_dpp: lanes of the banks in
+// BANKS take src moved by CTRL, the others keep old.
+template <int CTRL, int BANKS>
+__device__ __forceinline__ double dpp_merge(double old, double src) {
+  const long long o = __double_as_longlong(old), v = __double_as_longlong(src);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)v, CTRL, 0xF, BANKS, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(v >> 32), CTRL, 0xF, BANKS,
+                                             false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Reduce-scatter over a chain's 32 lanes (one half of the wave): on entry
+// every lane holds v[0..31], on return lane m (= lane % 32) holds the sum over
+// the 32 lanes of v[m].  Butterfly: at each level a lane keeps the half of its
+// values whose index bit equals its lane bit and adds the partner's copy of
+// that half — rows by v_permlane16_swap (no select: the swap delivers each
+// lane the partner's half it keeps), then xor 8 / 4 by row rotations and
+// xor 2 / 1 by quad permutes.  31 exchanges and 31 adds for 32 sums instead of
+// 5 of each per sum (half_sum_dpp).
+__device__ __forceinline__ double reduce_scatter32(const double (&v)[32]) {
+  // lane id by a volatile read: the lane-bit masks below are not hoisted out
+  // of the step loop (live across the pixel passes they spill)
+  int lid;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+  const int m = lid & 31;
+  double w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const long long X = __double_as_longlong(v[i]), Y = __double_as_longlong(v[i + 16]);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)X, (unsigned)Y, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(X >> 32), (unsigned)(Y >> 32),
+                                                     false, false);
+    // row 0: own v[i] + row 1's v[i]; row 1: row 0's v[i + 16] + own v[i + 16]
+    w[i] = __longlong_as_double(((long long)hi[0] << 32) | lo[0]) +
+           __longlong_as_double(((long long)hi[1] << 32) | lo[1]);
+  }
+  const bool b3 = m & 8, b2 = m & 4, b1 = m & 2, b0 = m & 1;
+  double u[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // xor 8: row_ror:8
+    const double keep = b3 ? w[i + 8] : w[i], send = b3 ? w[i] : w[i + 8];
+    u[i] = keep + dpp_move<0x128>(send);
+  }
+  double t[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {  // xor 4: banks 1, 3 from row_ror:4 (lane - 4), 0, 2 from :12
+    const double keep = b2 ? u[i + 4] : u[i], send = b2 ? u[i] : u[i + 4];
+    t[i] = keep + dpp_merge<0x124, 0xA>(dpp_move<0x12C>(send), send);
+  }
+  double z[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {  // xor 2: quad_perm [2,3,0,1]
+    const double keep = b1 ? t[i + 2] : t[i], send = b1 ? t[i] : t[i + 2];
+    z[i] = keep + dpp_move<0x4E>(send);
+  }
+  const double keep = b0 ? z[1] : z[0], send = b0 ? z[0] : z[1];
+  return keep + dpp_move<0xB1>(send);  // xor 1: quad_perm [1,0,3,2]
+}
 
 template <int IMG, int KMAX, int CT_ = RHMC_PK_CT>
 struct PixK {
@@ -232,6 +296,26 @@ struct PixK {
       columns<CT>(ci, simg, rtab, ctab, K, c, A0, A1, A2);
     if constexpr (NC % CT == 1) columns<1>(NC - 1, simg, rtab, ctab, K, c, A0, A1, A2);
     static_assert(NC % CT <= 1, "column passes");
+#if RHMC_PK_RS
+    // star k's sums land in lanes k, KMAX + k, 2 KMAX + k (phantom stars' A
+    // are zero)
+    static_assert(3 * KMAX <= 32, "one reduce-scatter slot per sum");
+    double v[32];
+#pragma unroll
+    for (int i = 0; i < 32; ++i)
+      v[i] = i < KMAX ? A0[i] : i < 2 * KMAX ? A1[i - KMAX] : i < 3 * KMAX ? A2[i - 2 * KMAX] : 0.0;
+    const double s0 = reduce_scatter32(v);
+    const int hb = (lane_id() & 32) + m;  // this lane, in the chain's half of the wave
+    const double s1 = __shfl(s0, hb + KMAX, kWave);  // lanes m >= K read past: unused
+    const double s2 = __shfl(s0, hb + 2 * KMAX, kWave);
+    gf = gx = gy = 0.0;
+    if (m < K) {
+      const KRStar st = tab[m];
+      gf = -s0 / st.f;                                      // :404
+      gx = -fma(kCtr - st.x, s0, s1) * lc.inv_var;          // :405
+      gy = -fma(kCtr - st.y, s0, s2) * lc.inv_var;          // :406
+    }
+#else
     gf = gx = gy = 0.0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -247,6 +331,7 @@ struct PixK {
         }
       }
     }
+#endif
   }
 };
 
@@ -267,7 +352,8 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x)
     simg[PK::img_index(e / IMG, e % IMG)] = a.Df[e];
   __syncthreads();
-  const int64_t wave = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
+  const int64_t wave =
+      (int64_t)blockIdx.x * W + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   if (PK::CPW * wave >= a.n_chains) return;
   const int lane = lane_id();
   const int h = lane / PK::LPC, m = lane % PK::LPC;
@@ -312,26 +398,33 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
     km_explicit_steps<SOLVER, 1, decltype(grad), true>(f, x, y, pf, px, py, own, tab,
                                                        a.n_steps, f_pos, c, lc, grad, st);
   }
+  // the output index again, from a volatile lane id: the one computed above,
+  // held across the step loop, spills
+  int lid;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+  const int64_t chain_o = PK::CPW * wave + lid / PK::LPC;
+  const int64_t e_o = (chain_o < a.n_chains ? chain_o : PK::CPW * wave) * 3 * (int64_t)a.K +
+                      3 * (int64_t)(own[0] ? lid % PK::LPC : 0);
   unsigned nf = 0u;
   if (own[0] && real) {
     if (!(isfinite(f[0]) && isfinite(x[0]) && isfinite(y[0]) && isfinite(pf[0]) &&
           isfinite(px[0]) && isfinite(py[0])))
       nf = RHMC_STATUS_NONFINITE;
-    a.q[e] = f[0];
-    a.q[e + 1] = x[0];
-    a.q[e + 2] = y[0];
-    a.p[e] = pf[0];
-    a.p[e + 1] = px[0];
-    a.p[e + 2] = py[0];
+    a.q[e_o] = f[0];
+    a.q[e_o + 1] = x[0];
+    a.q[e_o + 2] = y[0];
+    a.p[e_o] = pf[0];
+    a.p[e_o + 1] = px[0];
+    a.p[e_o + 2] = py[0];
   }
   unsigned all = st | nf;
 #pragma unroll
   for (int d = 16; d >= 1; d >>= 1) all |= (unsigned)__shfl_xor((int)all, d, kWave);
-  if (m == 0 && real) {
-    if (a.status) a.status[chain] = (int32_t)all;
+  if (lid % PK::LPC == 0 && chain_o < a.n_chains) {
+    if (a.status) a.status[chain_o] = (int32_t)all;
     if (a.fp_iters) {
-      a.fp_iters[2 * chain] = it_p;
-      a.fp_iters[2 * chain + 1] = it_q;
+      a.fp_iters[2 * chain_o] = it_p;
+      a.fp_iters[2 * chain_o + 1] = it_q;
     }
   }
 }
