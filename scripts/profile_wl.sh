@@ -9,6 +9,6 @@ for WL in "$@"; do
   mkdir -p "$OUT"
   timeout -k 10 600 python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu > "$OUT/bench.log" 2>&1 || exit $?
   tail -1 "$OUT/bench.log" > "$OUT/bench.json"
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu > "$OUT/rocprof.log" 2>&1 || exit $?
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 bench.py --workload $WL --steps ${STEPS:-3} --warmup 1 --no-cpu --no-e2e > "$OUT/rocprof.log" 2>&1 || exit $?
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read()); print(sys.argv[2], '%.4e' % d['value'], 'kernel_ms %.3f' % d['roofline']['kernel_ms'])" "$OUT/bench.json" $WL
 done
