@@ -17,8 +17,8 @@ Extra objects on the JSON line:
                 profiles/*.json (rocprofv3 PMC), or null.
   cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on the host cores, one
                 chain per process, bounded sample (rank 0, N=1 only).
-  end_to_end    (leapfrog mode) the host-buffer C-ABI call rhmc_leapfrog on the
-                same chains: H2D + fused launch + D2H, synchronous — the
+  end_to_end    (leapfrog mode, N=1) the host-buffer C-ABI call rhmc_leapfrog
+                on the same chains: H2D + fused launch + D2H, synchronous — the
                 PCIe-inclusive rate a NumPy caller sees; never `value`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2]
@@ -365,7 +365,7 @@ def main():
         "valu_active_frac": pmc.get("valu_active_frac"),
         "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
     }
-    if args.mode == "leapfrog" and not args.no_e2e:
+    if args.mode == "leapfrog" and not args.no_e2e and world == 1:
         out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)
     if rank == 0:
         out["cpu_baseline"] = cpu
