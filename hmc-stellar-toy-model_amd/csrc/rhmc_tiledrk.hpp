@@ -74,6 +74,13 @@ constexpr int TABK = 16;
 #define RHMC_KR_IMG_LDS 1
 #endif
 constexpr bool kImgLds = RHMC_KR_IMG_LDS;
+// Window-major variant without tables (C5): the three per-window sums go to a
+// per-chain LDS buffer and are reduced 8 windows at a time (0: three 32-lane
+// all-reduces per window).
+#ifndef RHMC_KR_DEFER
+#define RHMC_KR_DEFER 1
+#endif
+constexpr bool kDeferRed = RHMC_KR_DEFER;
 
 // This chain's half of a wave ballot (lanes 0-31 or 32-63).
 __device__ __forceinline__ bool half_any(bool v) {
@@ -98,6 +105,11 @@ struct TiledRK {
   // all-stars Lambda loop: fp32-image variant only (the fp64-image one would
   // spill: its window pixels take twice the registers)
   static constexpr bool kAll = TAB && kAllStarsTab && sizeof(DT) == sizeof(float);
+  // deferred sums: [8 windows x 3 sums] rows of RP doubles (32 lanes + pad:
+  // 16-byte aligned rows, rows 4 banks apart)
+  static constexpr bool kDefer = !TAB && kDeferRed;
+  static constexpr int RB = 8, RP = 34;
+  static constexpr int RED_DOUBLES = kDefer ? RB * 3 * RP : 0;
 
   // LDS: exp table, per-chain star tables, then (TAB) per-chain factor tables
   // and the image (DT [side][side], read by every window of the workgroup).
@@ -105,7 +117,7 @@ struct TiledRK {
     return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar) +
            (TAB ? (size_t)waves * CPW * K * 2 * side * sizeof(double) +
                       (kImgLds ? (size_t)side * side * sizeof(DT) : 0)
-                : 0);
+                : (size_t)waves * CPW * RED_DOUBLES * sizeof(double));
   }
   static __device__ __forceinline__ int origin(double v, int half, int omax) {
     if (!(fabs(v) < 1.0e7)) return 0;
@@ -302,13 +314,49 @@ struct TiledRK {
         }
         const double dxa = ((r0 + (double)(TR * a)) - sk.x) + 0.5;
         const double dyb = ((c0 + (double)b) - sk.y) + 0.5;
-        const double s0 = half_sum_dpp(a0);
-        const double s1 = half_sum_dpp(fma(dxa, a0, a1));
-        const double s2 = half_sum_dpp(fma(dyb, w0, w1));
-        if (m == kk) {
-          gf[t] = -s0;                              // :404
-          gx[t] = -s1 * sk.f * lc.inv_var;          // :405
-          gy[t] = -s2 * sk.f * lc.inv_var;          // :406
+        if constexpr (kDefer) {
+          // this lane's share of the window's three sums -> the chain's buffer;
+          // every RB windows (and after the slot's last) lane 3 w + c sums row
+          // (w, c) over the 32 lanes and lane kk0 + w collects window w's three
+          // (ftab is the buffer here)
+          double* row = ftab + (size_t)((kk % RB) * 3) * RP + m;
+          row[0] = a0;
+          row[RP] = fma(dxa, a0, a1);
+          row[2 * RP] = fma(dyb, w0, w1);
+          if (kk % RB == RB - 1 || k + 1 == K || kk == LPC - 1) {  // wave-uniform
+            wave_lds_sync();
+            const int kk0 = kk - kk % RB;
+            const double* rr = ftab + (size_t)(m < 3 * RB ? m : 0) * RP;
+            double v[LPC / 2];  // pairwise tree over the 32 lanes' shares
+#pragma unroll
+            for (int l = 0; l < LPC / 2; ++l) v[l] = rr[2 * l] + rr[2 * l + 1];
+#pragma unroll
+            for (int n = LPC / 4; n >= 1; n /= 2)
+#pragma unroll
+              for (int l = 0; l < n; ++l) v[l] = v[l] + v[l + n];
+            const double sum = v[0];
+            const int w = m - kk0;                  // this lane's window in the batch
+            const int src = (lane_id() & 32) + 3 * (w >= 0 && w < RB ? w : 0);
+            const double s0 = __shfl(sum, src, kWave);
+            const double s1 = __shfl(sum, src + 1, kWave);
+            const double s2 = __shfl(sum, src + 2, kWave);
+            if (w >= 0 && w <= kk - kk0) {
+              const double fk = tab[LPC * t + m].f;
+              gf[t] = -s0;                          // :404
+              gx[t] = -s1 * fk * lc.inv_var;        // :405
+              gy[t] = -s2 * fk * lc.inv_var;        // :406
+            }
+            wave_lds_sync();                        // reads done before the next batch
+          }
+        } else {
+          const double s0 = half_sum_dpp(a0);
+          const double s1 = half_sum_dpp(fma(dxa, a0, a1));
+          const double s2 = half_sum_dpp(fma(dyb, w0, w1));
+          if (m == kk) {
+            gf[t] = -s0;                            // :404
+            gx[t] = -s1 * sk.f * lc.inv_var;        // :405
+            gy[t] = -s2 * sk.f * lc.inv_var;        // :406
+          }
         }
       }
     }
@@ -727,8 +775,9 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   const int W = blockDim.x / kWave;
   const int slot = (threadIdx.x / kWave) * TK::CPW + h;  // chain slot in the workgroup
   KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * TK::KMAX;
+  // TAB: the chain's factor tables; otherwise its deferred-sum buffer
   double* ftab = lds + kExpTab + (size_t)W * TK::CPW * TK::KMAX * (sizeof(KRStar) / 8) +
-                 (size_t)slot * a.K * 2 * a.side;  // TAB only
+                 (TAB ? (size_t)slot * a.K * 2 * a.side : (size_t)slot * TK::RED_DOUBLES);
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
   const int K = a.K;
