@@ -213,13 +213,10 @@ struct TiledR {
   // exp(-(dx^2 + dy^2) c) by a few ulp).  A wave with a chain so far from its
   // window that a base exp or a ratio could leave the fp64 range
   // (|v0| or |w0| >= rec_vmax, or NaN) takes the direct factors instead.
-  static __device__ __forceinline__ void no_mark(int) {}
-  template <bool PROFG = false, class MARK = void (*)(int)>
   static __device__ __forceinline__ void factors_rec(const double* __restrict__ etab,
                                                      const Cache& k, double x, double y,
                                                      const LeanConsts& lc, double scale,
-                                                     double (&ex)[TR], double (&ey)[TC],
-                                                     MARK gmark = no_mark) {
+                                                     double (&ex)[TR], double (&ey)[TC]) {
 #if RHMC_FACT_REC
     const int lane = lane_id();
     const int m = lane % LPC;
@@ -233,10 +230,6 @@ struct TiledR {
       const double lin = (b < 2) ? fma(2.0, z, 1.0) : fma(8.0, z, 16.0);
       const double t = ((b & 1) ? lin : z * z) * -c;
       const double e = exp_neg(t, etab);
-      if constexpr (PROFG) {
-        asm volatile("" ::"v"(e));
-        gmark(4);
-      }
       const double ex0 = row_bcast<0>(e), g0 = row_bcast<1>(e);
       const int src = (lane & ~(LPC - 1)) + 4 * b;
       const double ey0 = __shfl(e, src + 2, kWave) * (lc.inv_norm * scale);
@@ -296,8 +289,7 @@ struct TiledR {
   // factors carry f (fey = f ey serves Lambda and both sums), so no separate
   // f ex row factors are held: 14 VGPRs and 7 products fewer.
   // PROFG (tools only): fenced clock reads split the gradient into gp[3] window
-  // check, gp[4] range check + exp, gp[0] factor broadcasts + recurrences,
-  // gp[1] pixel loop, gp[2] moments + reductions.
+  // check, gp[0] PSF factors, gp[1] pixel loop, gp[2] moments + reductions.
   template <bool PROFG = false>
   static __device__ __forceinline__ void partial(const double* __restrict__ etab,
                                                  const DT* __restrict__ sD, Cache& k, double f,
@@ -321,7 +313,7 @@ struct TiledR {
     gmark(3);
     const double r0 = k.r0, c0 = k.c0;
     double ex[TR], ey[TC];
-    factors_rec<PROFG>(etab, k, x, y, lc, f, ex, ey, gmark);  // ey carries f
+    factors_rec(etab, k, x, y, lc, f, ex, ey);  // ey carries f
     gmark(0);
 
     // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
@@ -443,7 +435,7 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
   TL::init(cache);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
-  long long prof[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   k1_steps<PROF, TL::LPC>(f, x, y, pf, px, py, a.n_steps, (double)(IMG - 1), c, lc,
                  [&](double f_, double x_, double y_, double& gf, double& gx, double& gy) {
                    TL::template gradient<PROF>(lds, simg, cache, f_, x_, y_, c, lc, gf, gx, gy,
@@ -460,7 +452,6 @@ leapfrog_k1_tiledr(LeapArgsK1 a) {
     py = prof[5] / ns;  // pixel loop (prof[6], moments + reductions: it_p)
     it_p = (int)(prof[6] / ns);
     it_q = (int)(prof[7] / ns);  // window check
-    st = (unsigned)(prof[8] / ns);  // ok ballot + the exp
   }
 
   if ((lane % TL::LPC) == 0 && real) {

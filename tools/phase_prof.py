@@ -38,10 +38,9 @@ if kern.startswith("profr"):
     print("%s n=%d cycles/step: gradient %.0f  kicks+p-loop %.0f  q-loop %.0f  flux+tail %.0f"
           "  total %.0f" % (kern, n, ph[0], ph[1], ph[2], ph[3], sum(ph)))
     itn = it.cpu().numpy().astype(float)
-    g5 = [itn[:, 1].mean(), st.cpu().numpy().astype(float).mean(), pp[:, 1].mean(),
-          pp[:, 2].mean(), itn[:, 0].mean()]
-    print("  gradient split: window check %.0f  range check + exp %.0f  broadcasts + "
-          "recurrences %.0f  pixel loop %.0f  moments + reductions %.0f" % tuple(g5))
+    g4 = [itn[:, 1].mean(), pp[:, 1].mean(), pp[:, 2].mean(), itn[:, 0].mean()]
+    print("  gradient split: window check %.0f  PSF factors %.0f  pixel loop %.0f  "
+          "moments + reductions %.0f" % tuple(g4))
 else:
     a = it.cpu().numpy().astype(float)
     print("%s n=%d cycles/step: gradient %.0f  rest %.0f  total %.0f" % (
