@@ -189,9 +189,13 @@ struct PixK {
 #pragma unroll
     for (int q = 0; q < N; ++q) {
       const double wj = ((double)(cg + 16 * (ci0 + q)) + 0.5) - kCtr;
+      // all KMAX slots: a phantom star's (k >= K) table entries are zero, so its
+      // sums stay zero (the guard on the runtime K compiles to selects: 180 per
+      // gradient; kept only for the two-column HMC_random variant, where
+      // dropping it spills a loop invariant)
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
-        if (k < K) {  // wave-uniform
+        if (CT == 3 || k < K) {
           A0[k] = fma(fey[q][k], c0[q][k], A0[k]);
           A1[k] = fma(fey[q][k], c1[q][k], A1[k]);
           A2[k] = fma(wj * fey[q][k], c0[q][k], A2[k]);

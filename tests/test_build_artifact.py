@@ -1,7 +1,6 @@
 """CPU checks of the shipped librhmc.so code object (gfx950): the hot leapfrog
 kernels must not touch scratch memory (register spills turn the VALU-bound
-loop into a memory-bound one — a one-step `hipcc -shared` build once did),
-apart from the pixel-major kernels' one spilled loop invariant."""
+loop into a memory-bound one — a one-step `hipcc -shared` build once did)."""
 import os
 import re
 import shutil
@@ -47,8 +46,4 @@ def test_gfx950_code_object_present_and_hot_kernels_spill_free(tmp_path):
         if "win_kernel" in name:
             continue        # windowed kernel: a few scratch words from exp/pow (measured, small)
         n = sum("scratch_" in l for l in funcs[name])
-        # the pixel-major implicit kernels sit at 255 VGPRs: one spilled
-        # loop-invariant (one store before the step loop, one load per step in
-        # the flux metric); the failure this guards against is hundreds
-        limit = 4 if "leapfrog_pk" in name else 0
-        assert n <= limit, "%s uses scratch (%d instructions)" % (name, n)
+        assert n == 0, "%s uses scratch (%d instructions)" % (name, n)
