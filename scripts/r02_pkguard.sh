@@ -1,6 +1,6 @@
 #!/bin/bash
-# GPU suite, then the pixel-major kernel without the runtime-K guard on the
-# per-star accumulation (new) vs with it (prev): C3 implicit and explicit modes.
+# GPU suite, then a pixel-major kernel change (new) against the previous build
+# (prev): C3 implicit x3 and the explicit modes (used for the guard removal and the row peel).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 timeout -k 10 300 python3 -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
