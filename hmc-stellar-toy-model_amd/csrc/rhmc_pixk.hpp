@@ -190,16 +190,13 @@ struct PixK {
     for (int q = 0; q < N; ++q) {
       const double wj = ((double)(cg + 16 * (ci0 + q)) + 0.5) - kCtr;
       // all KMAX slots: a phantom star's (k >= K) table entries are zero, so its
-      // sums stay zero (the guard on the runtime K compiles to selects: 180 per
-      // gradient; kept only for the two-column HMC_random variant, where
-      // dropping it spills a loop invariant)
+      // sums stay zero (a guard on the runtime K compiled to 180 selects per
+      // gradient)
 #pragma unroll
       for (int k = 0; k < KMAX; ++k) {
-        if (CT == 3 || k < K) {
-          A0[k] = fma(fey[q][k], c0[q][k], A0[k]);
-          A1[k] = fma(fey[q][k], c1[q][k], A1[k]);
-          A2[k] = fma(wj * fey[q][k], c0[q][k], A2[k]);
-        }
+        A0[k] = fma(fey[q][k], c0[q][k], A0[k]);
+        A1[k] = fma(fey[q][k], c1[q][k], A1[k]);
+        A2[k] = fma(wj * fey[q][k], c0[q][k], A2[k]);
       }
     }
   }
@@ -345,9 +342,9 @@ struct PixK {
 template <int IMG, int KMAX, int SOLVER = RHMC_SOLVER_IMPLICIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_pk(LeapArgsKR a, int f_pos) {
-  // HMC_random keeps a little more state across the gradient: two columns
-  // per pass there (three spill)
-  using PK = PixK<IMG, KMAX, (SOLVER == kSolverHmcRandom ? 2 : RHMC_PK_CT)>;
+  // (HMC_random ran two columns per pass until the unguarded accumulation
+  // freed the registers three need)
+  using PK = PixK<IMG, KMAX, RHMC_PK_CT>;
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;
   exp_tab_fill(lds);
