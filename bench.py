@@ -10,24 +10,36 @@ resident in HBM and carry over from launch to launch.
 value = total chain-leapfrog-steps over all ranks / max-over-ranks wall time.
 
 Extra objects on the JSON line:
-  roofline      algorithmic HBM bytes per chain-step (SURVEY §8(d):
-                2*N_pix*8 + 4*3K*8 = 36,960 B at C2) x chain-steps per launch
-                / average launch time, HIP events on the launch stream;
-                peak 8.0 TB/s.  `traffic` = measured HBM bytes per launch from
-                profiles/*.json (rocprofv3 PMC), or null.
-  cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on the host cores, one
-                chain per process, bounded sample (rank 0, N=1 only).
+  roofline      the binding roof, fp64 VALU: executed fp64 FLOP per chain-step
+                (rocprofv3 PMC, profiles/pmc_<wl>.json) x chain-steps per
+                launch / the launch's HIP-event time on the launch stream,
+                over the 78.6 TF/s fp64 vector peak; `traffic` = measured HBM
+                bytes per launch (PMC), `hbm_measured_frac` its rate over
+                8 TB/s; `alg_model` = SURVEY §8(d)'s algorithmic-bytes model
+                (above the HBM peak by construction: D lives in LDS/VGPRs).
+  cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on every core of the
+                affinity mask, one chain per worker process, ~10 s per worker
+                (rank 0, N=1 only).
   end_to_end    (leapfrog mode, N=1) the host-buffer C-ABI call rhmc_leapfrog
                 on the same chains: H2D + fused launch + D2H, synchronous — the
                 PCIe-inclusive rate a NumPy caller sees; never `value`.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--workload C2]
-       (N>1: launched by torch.distributed.run, one rank per GPU)
+  N > 1 without WORLD_SIZE in the environment: this process starts N rank
+  processes of itself (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, rank r on
+  GPU r) before touching a GPU, relays rank 0's JSON line and fails if any
+  rank fails.  Under torch.distributed.run (WORLD_SIZE set) each process is
+  one rank; --gpus must then equal WORLD_SIZE.
+  --dry-run: rendezvous the ranks and print the sharding plan without
+  touching a GPU (the CPU tests use it).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -56,27 +68,51 @@ def _cpu_worker(args):
     return time.perf_counter() - t
 
 
-def cpu_baseline(wl, seconds_target=15.0):
-    """Time the NumPy port, one chain per process (multiprocessing.Pool)."""
+def cpu_quota_cores():
+    """CPUs the cgroup lets this process use (cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            quota, period = open(path).read().split()[:2]
+            if quota != "max":
+                return float(quota) / float(period)
+        except (OSError, ValueError):
+            pass
+    try:
+        quota = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        if quota > 0:
+            return quota / period
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def cpu_baseline(wl, seconds_per_worker=10.0):
+    """Time the NumPy port on every host core this process may run on: one
+    chain per worker process (multiprocessing.Pool, OMP_NUM_THREADS=1), one
+    worker per core of the affinity mask, each running >= ~10 s."""
     import multiprocessing as mp
     os.environ["OMP_NUM_THREADS"] = "1"
     try:
-        cores = len(os.sched_getaffinity(0))
+        avail = len(os.sched_getaffinity(0))
     except AttributeError:
-        cores = os.cpu_count()
-    cores = max(1, min(cores, 16))
+        avail = os.cpu_count()
+    workers = max(1, avail)
+    quota = cpu_quota_cores()
     par = dict(wl.params)
     par["rows"] = par["cols"] = wl.D.shape[0]
-    # calibrate one chain on this core
+    # calibrate one chain on one idle core
     t = _cpu_worker((wl.D, par, wl.q0[0], wl.p0[0], 20))
     per_step = t / 20
-    nsteps = max(20, int(seconds_target / per_step / 2))
+    # a cgroup quota below the worker count stretches every worker's wall time
+    share = min(1.0, quota / workers) if quota else 1.0
+    nsteps = max(20, int(seconds_per_worker * share / per_step))
     jobs = [(wl.D, par, wl.q0[c % wl.n_chains], wl.p0[c % wl.n_chains], nsteps)
-            for c in range(2 * cores)]
+            for c in range(workers)]
     ctx = mp.get_context("fork")
     t0 = time.perf_counter()
-    with ctx.Pool(cores) as pool:
-        pool.map(_cpu_worker, jobs)
+    with ctx.Pool(workers) as pool:
+        worker_s = pool.map(_cpu_worker, jobs)
     wall = time.perf_counter() - t0
     total = len(jobs) * nsteps
     try:
@@ -84,11 +120,64 @@ def cpu_baseline(wl, seconds_target=15.0):
                  if l.startswith("model name")][0]
     except Exception:
         model = "unknown"
-    return {"value": total / wall, "unit": "chain-leapfrog-steps/s", "cores": cores,
-            "kind": "port",
+    return {"value": total / wall, "unit": "chain-leapfrog-steps/s", "cores": workers,
+            "cores_available": avail, "cores_used": workers, "cpu_quota_cores": quota,
+            "kind": "port", "worker_seconds_min": min(worker_s),
+            "one_core_value": 1.0 / per_step,
             "sample": "%d chains x %d steps of %s geometry, NumPy port of RHMC_single_step "
-                      "(oracle/rhmc_ref.py), one chain per process, %s"
-                      % (len(jobs), nsteps, wl.name, model)}
+                      "(oracle/rhmc_ref.py), one chain per worker process on each of the %d "
+                      "cores of the affinity mask, %s"
+                      % (len(jobs), nsteps, wl.name, workers, model)}
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(n):
+    """Start n rank processes of this script (one per GPU) and wait for them.
+
+    Called before anything touches a GPU (no torch import here).  Each child
+    gets RANK = LOCAL_RANK = r, WORLD_SIZE = n and a 127.0.0.1 rendezvous;
+    rank 0's stdout (the JSON line) is relayed, the other ranks' stdout goes
+    to stderr.  If a rank fails, the others are terminated and the exit code
+    is non-zero."""
+    port = _free_port()
+    procs, outs = [], []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        out = tempfile.TemporaryFile(mode="w+")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env, stdout=out))
+        outs.append(out)
+    rc = 0
+    live = set(range(n))
+    while live:
+        for r in sorted(live):
+            code = procs[r].poll()
+            if code is None:
+                continue
+            live.discard(r)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                sys.stderr.write("bench.py: rank %d exited with %d; stopping the others\n"
+                                 % (r, code))
+                for k in live:
+                    procs[k].terminate()
+        time.sleep(0.05)
+    for r, out in enumerate(outs):
+        out.seek(0)
+        text = out.read()
+        (sys.stdout if r == 0 else sys.stderr).write(text)
+        out.close()
+    sys.stdout.flush()
+    return rc
 
 
 def load_pmc(workload):
@@ -164,7 +253,8 @@ def bench_datagen(args, wl, P, ctx, dev, stream, world, rank):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) on this node; default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--workload", default="C2")
@@ -187,9 +277,24 @@ def main():
     ap.add_argument("--mh-iter", type=int, default=10)
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
     ap.add_argument("--n-real", type=int, default=1000)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="rendezvous the ranks and print the sharding plan; no GPU work")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n < 1:
+            raise SystemExit("bench.py: --gpus must be >= 1")
+        if n > 1:
+            # one process per GPU: start the ranks before any GPU call here
+            return spawn_ranks(n)
+        world = 1
+    else:
+        world = int(env_world)
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit("bench.py: --gpus %d disagrees with WORLD_SIZE=%d"
+                             % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -204,6 +309,12 @@ def main():
         wl.q0, wl.p0 = wl.q0[lo:hi].copy(), wl.p0[lo:hi].copy()
     else:
         wl = workloads.make(args.workload, n_chains=args.chains, seed_offset=rank)
+    # RHMC_BENCH_DEVICE pins every rank to one device (rehearsing the N-rank
+    # path on a one-GPU box); by default rank r of a node uses GPU r.
+    gpu = int(os.environ.get("RHMC_BENCH_DEVICE", local_rank))
+    total_chains = args.global_chains or wl.n_chains * world
+    if args.dry_run:
+        return dry_run(args, wl, world, rank, gpu, total_chains)
     # CPU baseline first: forked workers must not inherit an initialised GPU.
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and args.mode == "leapfrog":
@@ -215,9 +326,10 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    # RHMC_BENCH_DEVICE pins every rank to one device (rehearsing the N-rank
-    # path on a one-GPU box); by default rank r of a node uses GPU r.
-    gpu = int(os.environ.get("RHMC_BENCH_DEVICE", local_rank))
+    ndev = torch.cuda.device_count()
+    if gpu >= ndev:
+        raise SystemExit("bench.py: rank %d wants GPU %d but %d are visible"
+                         % (rank, gpu, ndev))
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
 
@@ -291,20 +403,18 @@ def main():
                 "q_loop_mean": float(iters[:, 1].mean() / max(leap, 1)),
                 "p_loop_cap_chains": int(((stat & capi.STATUS_PLOOP_CAP) != 0).sum()),
                 "q_loop_cap_chains": int(((stat & capi.STATUS_QLOOP_CAP) != 0).sum()),
-                "flux_wall_chains": int(((stat & capi.STATUS_REFLECT_F) != 0).sum())}
+                "flux_wall_chains": int(((stat & capi.STATUS_REFLECT_F) != 0).sum()),
+                # a reflection within 1e-12 of its wall (f_lim, 0,
+                # R-1; sampler_RHMC.py:554-564) can legitimately flip the other
+                # way on a rounding difference — reported separately
+                "near_wall_chains": int(((stat & capi.STATUS_NEAR_WALL) != 0).sum()),
+                "near_wall_frac": float(((stat & capi.STATUS_NEAR_WALL) != 0).mean())}
 
     steps_per_launch = leap * (args.mh_iter if args.mode == "mh" else 1)
     chain_steps = wl.n_chains * steps_per_launch
-    total_chains = args.global_chains or wl.n_chains * world
     value = total_chains * steps_per_launch * args.steps / wall
-    npix = wl.D.size
-    bpu = alg_bytes_per_step(npix, wl.K)
-    achieved = bpu * chain_steps / (launch_ms * 1e-3) / 1e9
     # PMC summaries describe the implicit leapfrog kernel only
     pmc = load_pmc(wl.name) if args.mode == "leapfrog" else {}
-    traffic = pmc.get("hbm_bytes_per_launch")
-    if traffic is not None and pmc.get("chain_steps_per_dispatch") not in (None, chain_steps):
-        traffic = traffic * chain_steps / pmc["chain_steps_per_dispatch"]
     metric = "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X"
     if wl.name != "C2" or args.chains or args.global_chains or args.mode != "leapfrog":
         # not the headline configuration: name what was run
@@ -332,38 +442,9 @@ def main():
                    "solver": (args.solver if args.mode == "integrate" else
                               "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},
-        # The contract's roofline object prices the reference's ALGORITHMIC
-        # bytes (D read by both gradients + q/p in/out).  The
-        # kernels keep D in LDS and the window pixels in VGPRs, so that model
-        # is not a bound here (frac > 1 by construction, binding=False); the
-        # measured HBM rate is traffic / kernel time (`measured_gbs`) and the
-        # roof that binds is `roofline_fp64_valu` below.
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "binding": False,
-                     "binding_roof": "roofline_fp64_valu",
-                     "note": "achieved = algorithmic-model bytes (2*N_pix*8 + 4*3K*8 per "
-                             "chain-step) / kernel time; the image is LDS/VGPR-resident, so "
-                             "this model exceeds physical HBM traffic and does not bind",
-                     "measured_gbs": (None if traffic is None
-                                      else traffic / (launch_ms * 1e-3) / 1e9),
-                     "alg_bytes_per_chain_step": bpu, "kernel_ms": launch_ms,
-                     "alg_model_fp64_tflops": alg_flops_per_step(npix, wl.K) * chain_steps
-                     / (launch_ms * 1e-3) / 1e12},
+        "roofline": roofline(pmc, wl, chain_steps, launch_ms),
         "nonfinite_chains": nonfinite,
         "fixed_point_iters_per_step": fp_stats,
-    }
-    # The image is LDS-resident, so the algorithmic-HBM fraction above exceeds
-    # 1; the physically binding roof is FP64 VALU issue: executed fp64 flops per
-    # chain-step (PMC, profiles/pmc_<wl>.json) x rate / 78.6 TF/s.
-    fpc = pmc.get("fp64_flops_per_chain_step")
-    out["roofline_fp64_valu"] = None if fpc is None else {
-        "bound": "valu-fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
-        "achieved": fpc * chain_steps / (launch_ms * 1e-3) / 1e12,
-        "frac": fpc * chain_steps / (launch_ms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
-        "executed_fp64_flops_per_chain_step": fpc,
-        "valu_active_frac": pmc.get("valu_active_frac"),
-        "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
     }
     if args.mode == "leapfrog" and not args.no_e2e and world == 1:
         out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)
@@ -373,6 +454,75 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def roofline(pmc, wl, chain_steps, launch_ms):
+    """The roof that binds the dominant kernel: fp64 VALU issue.
+
+    The image is LDS-resident and each chain's window pixels sit in VGPRs, so
+    HBM traffic is ~0.7 MB per launch — HBM does not bound these kernels.
+    achieved = executed fp64 FLOP per chain-step (rocprofv3 PMC of the same
+    kernel, profiles/pmc_<wl>.json: 64 lanes x (2 FMA + MUL + ADD) per
+    instruction) x chain-steps per launch / the launch's HIP-event time;
+    peak = 78.6 TF/s fp64 vector.  `traffic` = measured HBM bytes per launch
+    (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction), `hbm_measured_frac` its
+    rate over 8 TB/s.  `alg_model` keeps SURVEY §8(d)'s algorithmic-bytes model
+    (D read by both gradients + q/p in/out per chain-step), which exceeds the
+    HBM peak by construction because D never leaves the chip."""
+    s = launch_ms * 1e-3
+    traffic = pmc.get("hbm_bytes_per_launch")
+    per = pmc.get("chain_steps_per_dispatch")
+    if traffic is not None and per not in (None, chain_steps):
+        traffic = traffic * chain_steps / per
+    fpc = pmc.get("fp64_flops_per_chain_step")
+    npix = wl.D.size
+    bpu = alg_bytes_per_step(npix, wl.K)
+    alg_gbs = bpu * chain_steps / s / 1e9
+    achieved = None if fpc is None else fpc * chain_steps / s / 1e12
+    return {
+        "bound": "valu-fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
+        "achieved": achieved,
+        "frac": None if achieved is None else achieved / FP64_PEAK_TFLOPS,
+        "traffic": traffic,
+        "kernel_ms": launch_ms,
+        "chain_steps_per_launch": chain_steps,
+        "executed_fp64_flops_per_chain_step": fpc,
+        "valu_active_frac": pmc.get("valu_active_frac"),
+        "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
+        "pmc_source": ("profiles/pmc_%s.json (%s)" % (wl.name.lower(), pmc.get("kernel", "?"))
+                       if pmc else None),
+        "hbm_measured_gbs": None if traffic is None else traffic / s / 1e9,
+        "hbm_measured_frac": None if traffic is None else traffic / s / 1e9 / HBM_PEAK_GBS,
+        "alg_model": {
+            "bound": "hbm", "unit": "GB/s", "peak": HBM_PEAK_GBS,
+            "bytes_per_chain_step": bpu, "achieved": alg_gbs, "frac": alg_gbs / HBM_PEAK_GBS,
+            "fp64_tflops": alg_flops_per_step(npix, wl.K) * chain_steps / s / 1e12,
+            "note": "SURVEY 8(d) algorithmic model (2*N_pix*8 + 4*3K*8 B per chain-step); "
+                    "exceeds the HBM peak by construction: the image is read from "
+                    "LDS/VGPRs, not HBM, so this is not a bound"},
+    }
+
+
+def dry_run(args, wl, world, rank, gpu, total_chains):
+    """The sharding plan every rank would run, gathered over gloo: no GPU
+    work.  Rank 0 prints one JSON line."""
+    plan = {"rank": rank, "gpu": gpu, "chains": int(wl.n_chains),
+            "first_state": [float(v) for v in wl.q0[0]]}
+    plans = [plan]
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+        plans = [None] * world
+        dist.all_gather_object(plans, plan)
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "workload": wl.name,
+                          "config": {"chains_per_gpu": int(wl.n_chains),
+                                     "total_chains": int(total_chains),
+                                     "parallelism": "chain-sharded x%d" % world},
+                          "ranks": plans}), flush=True)
+    return 0
 
 
 def end_to_end(ctx, P, q, p, wl, leap, reps=3):
@@ -393,4 +543,4 @@ def end_to_end(ctx, P, q, p, wl, leap, reps=3):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main() or 0)

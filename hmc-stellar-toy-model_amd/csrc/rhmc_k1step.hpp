@@ -44,6 +44,19 @@ struct FluxMetric {
   double prior;  // alpha/f (use_prior)                                    (:408-409)
 };
 
+// Arguments of the single-star kernels (register-window, lane-group).
+struct LeapArgsK1 {
+  double* q;
+  double* p;
+  int32_t* fp_iters;
+  int32_t* status;
+  const double* D;
+  const float* Df;   // D in fp32 when exact (ctx->img_f32), else nullptr
+  int64_t n_chains;
+  int n_steps, rows, cols, pad;
+  Consts c;
+};
+
 __device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
                                                   const LeanConsts& l) {
   FluxMetric m;
@@ -55,7 +68,7 @@ __device__ __forceinline__ FluxMetric flux_metric(double f, const Consts& c,
   const double fl = low ? l.f_low : f;
   const double u = rcp_nr(fl);
   m.s = u * fma(l.Bg2, u, l.inv_g1);
-  const double t2 = low ? 0.0 : (u * u) * fma(2.0 * l.Bg2, u, l.inv_g1) * rcp_nr(m.s);
+  const double t2 = low ? 0.0 : (u * u) * fma(l.two_Bg2, u, l.inv_g1) * rcp_nr(m.s);
   const double t1 = -m.A * (ib * ib);
   m.mterm = (t1 + 2.0 * t2) / 2.0;
   m.prior = c.use_prior ? c.alpha * (low ? rcp_nr(f) : u) : 0.0;
@@ -179,14 +192,17 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (f < c.f_lim) {                           // :554-564
         pf = -pf;
         st |= RHMC_STATUS_REFLECT_F;
+        if (f >= c.near_f) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (x < 0.0 || x > edge) {
         px = -px;
         st |= RHMC_STATUS_REFLECT_XY;
+        if (near_edge(x, edge)) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (y < 0.0 || y > edge) {
         py = -py;
         st |= RHMC_STATUS_REFLECT_XY;
+        if (near_edge(y, edge)) st |= RHMC_STATUS_NEAR_WALL;
       }
     }
     if (s == n_steps) {

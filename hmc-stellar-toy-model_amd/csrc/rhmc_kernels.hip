@@ -29,15 +29,11 @@
 #include "rhmc.h"
 #include "rhmc_datagen.hpp"
 #include "rhmc_mh.hpp"
-#include "rhmc_tiled.hpp"
-#include "rhmc_tiled2.hpp"
-#include "rhmc_tiledk.hpp"
 #include "rhmc_tiledl.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
 #include "rhmc_mhk1.hpp"
 #include "rhmc_pixk.hpp"
-#include "rhmc_tiledw.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 
@@ -223,14 +219,17 @@ __device__ __forceinline__ void run_steps(StarState& s, bool owner, int n_steps,
       if (s.f < c.f_lim) {
         s.pf = -s.pf;
         st |= RHMC_STATUS_REFLECT_F;
+        if (s.f >= c.near_f) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (s.x < 0.0 || s.x > (double)(rows - 1)) {
         s.px = -s.px;
         st |= RHMC_STATUS_REFLECT_XY;
+        if (near_edge(s.x, (double)(rows - 1))) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (s.y < 0.0 || s.y > (double)(cols - 1)) {
         s.py = -s.py;
         st |= RHMC_STATUS_REFLECT_XY;
+        if (near_edge(s.y, (double)(cols - 1))) st |= RHMC_STATUS_NEAR_WALL;
       }
     }
     if (step == n_steps) break;
@@ -344,36 +343,6 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
                        [&](double f, double x, double y, double& gf, double& gx, double& gy) {
                          gradient<MAXK>(sD, tab, K, f, x, y, g, c, true, gf, gx, gy);
                        });
-  store_chain(a, chain, base, owner, s, it_p, it_q, st);
-}
-
-// Multi-star tiled kernel (2 <= K <= KMAX <= 16, IMG x IMG image, IMG in {32, 48}).
-template <int IMG, int KMAX>
-__global__ void __launch_bounds__(256) leapfrog_tiledk_kernel(LeapArgs a) {
-  using TK = TiledK<IMG, KMAX>;
-  extern __shared__ double lds[];
-  const int W = blockDim.x / kWave;
-  for (int e = threadIdx.x; e < TK::NPIX; e += blockDim.x) {
-    const int r = e / IMG, cc = e - (e / IMG) * IMG;
-    lds[Tiled<IMG>::tiled_index(r, cc)] = a.D[e];
-  }
-  __syncthreads();
-  const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
-  if (chain >= a.n_chains) return;
-  const int K = a.K;
-  double* tab = lds + TK::NPIX + (threadIdx.x / kWave) * TK::TAB;
-  const double* sDl = lds + lane_id();
-  const Consts& c = a.c;
-  const LeanConsts lc = lean_consts(c);
-  const bool owner = lane_id() < K;
-  int64_t base;
-  StarState s = load_chain(a, chain, K, owner, base);
-  int it_p = 0, it_q = 0;
-  unsigned st = 0u;
-  run_steps<false>(s, owner, a.n_steps, IMG, IMG, c, it_p, it_q, st,
-                   [&](double f, double x, double y, double& gf, double& gx, double& gy) {
-                     TK::gradient(sDl, tab, K, f, x, y, c, lc, gf, gx, gy);
-                   });
   store_chain(a, chain, base, owner, s, it_p, it_q, st);
 }
 
@@ -781,31 +750,21 @@ struct rhmc_ctx {
   size_t mh_scratch_bytes = 0;
   int max_lds = 0;
   int n_cu = 0;
+  int kernel = RHMC_KERNEL_AUTO;   // RHMC_OPT_KERNEL
+  int mh_fused = 1;                // RHMC_OPT_MH_FUSED
 };
 
 namespace {
 
-constexpr bool kDefaultTiled2 = true;
+// Kernel selection is a context option (RHMC_OPT_KERNEL, rhmc.h); the parity
+// tests run the same inputs through every family.  GENERIC / WINDOWED force
+// the one-wave-per-chain kernels for every call.
+bool per_wave_forced(const rhmc_ctx* ctx) {
+  return ctx->kernel == RHMC_KERNEL_GENERIC || ctx->kernel == RHMC_KERNEL_WINDOWED;
+}
+bool force_windowed(const rhmc_ctx* ctx) { return ctx->kernel == RHMC_KERNEL_WINDOWED; }
 
-// RHMC_KERNEL=generic / =windowed force a kernel family (the parity tests run
-// the same inputs through every path).
-bool force_generic() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strcmp(e, "generic") == 0;
-}
-bool force_windowed() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strcmp(e, "windowed") == 0;
-}
-// Single-star kernel variant: "tiled1" (one chain per wave) or "tiled2" (two).
-bool use_tiled2() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  if (e && std::strcmp(e, "tiled1") == 0) return false;
-  if (e && std::strcmp(e, "tiled2") == 0) return true;
-  return kDefaultTiled2;
-}
-
-// The 32-pixel windows (rhmc_tiledw.hpp, rhmc_windowed.hpp) drop pixel
+// The 32-pixel windows (rhmc_windowed.hpp) drop pixel
 // centres >= 15.5 px from a star; exact to fp64 only while their PSF factor
 // exp(-15.5^2 / (2 sigma^2)) <= 2^-70, i.e. sigma <= 1.574 px (reference: 1.487).
 bool window_exact(const Consts& c) { return 15.5 * 15.5 * c.inv_two_sig2 >= 48.5; }
@@ -816,14 +775,6 @@ int window_unsupported() {
               "that needs the windowed kernels (K > 16 or image larger than LDS)");
 }
 
-// Single-star kernel selection (RHMC_KERNEL): tiledr* = register-window
-// kernel (the default), tiledw / tiledw32 = LDS-operand window kernel with 16 /
-// 32 lanes per chain, tiled1 / tiled2 = full-image kernels.
-bool force_full_image_k1() {
-  const char* e = std::getenv("RHMC_KERNEL");
-  return e && std::strncmp(e, "tiledw", 6) != 0 && std::strncmp(e, "tiledr", 6) != 0 &&
-         std::strncmp(e, "tiledl", 6) != 0 && std::strncmp(e, "tiled", 5) == 0;
-}
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
 constexpr int kMaxK = 64;          // windowed kernel: lanes = stars
@@ -834,7 +785,7 @@ bool use_windowed(const rhmc_ctx* ctx, int K) {
   if (K > kMaxKGeneric) return true;
   const size_t need = ((size_t)ctx->rows * ctx->cols + table_doubles(K, ctx->rows, ctx->cols)) *
                       sizeof(double);
-  return need > (size_t)ctx->max_lds || force_windowed();
+  return need > (size_t)ctx->max_lds || force_windowed(ctx);
 }
 
 // Windowed kernels: W waves per workgroup, LDS = W * tables.
@@ -886,6 +837,7 @@ int make_consts(const rhmc_params* P, Consts* c) {
   c->inv_gff2 = 1.0 / c->g_ff2;
   c->inv_g1 = 1.0 / c->g1;
   c->Bg2 = c->B / c->g2;
+  c->two_Bg2 = 2.0 * c->Bg2;
   c->inv_gxx = 1.0 / c->g_xx;
   c->inv_two_sig2 = 1.0 / c->two_sig2;
   c->inv_norm = 1.0 / c->psf_norm;
@@ -903,6 +855,7 @@ int make_consts(const rhmc_params* P, Consts* c) {
     vm = std::fmin(vm, 700.0 / (8.0 * ci) - 34.0);
     c->rec_vmax = (ci > 0.0 && vm > 0.0) ? vm : 0.0;
   }
+  c->near_f = P->f_lim - 0x1p-40 * std::fmax(1.0, std::fabs(P->f_lim));
   c->counter_max = P->counter_max;
   c->use_prior = P->use_prior != 0;
   c->use_Vc = P->use_Vc != 0;
@@ -982,56 +935,6 @@ struct EnergyLaunch {
 };
 
 
-template <int IMG>
-int launch_tiled2(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  int W = 4;
-  size_t lds = Tiled2<IMG>::lds_doubles(W) * sizeof(double);
-  while (lds > (size_t)ctx->max_lds && W > 1) {
-    W >>= 1;
-    lds = Tiled2<IMG>::lds_doubles(W) * sizeof(double);
-  }
-  const int64_t waves = (a.n_chains + 1) / 2;
-  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL(leapfrog_k1_tiled2<IMG>, grid, block, lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
-}
-
-template <int IMG>
-int launch_tiled(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  if (use_tiled2()) return launch_tiled2<IMG>(ctx, a, s);
-  int W = 4;
-  size_t lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
-  while (lds > (size_t)ctx->max_lds && W > 1) {
-    W >>= 1;
-    lds = Tiled<IMG>::lds_doubles(W) * sizeof(double);
-  }
-  const dim3 grid((unsigned)((a.n_chains + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL(leapfrog_k1_tiled<IMG>, grid, block, lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
-}
-
-template <int IMG, int LPC, bool PROF = false>
-int launch_tiledw_lpc(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  using TL = TiledW<IMG, LPC>;
-  int W = 4;
-  size_t lds = TL::lds_doubles(W) * sizeof(double);
-  while (lds > (size_t)ctx->max_lds && W > 1) {
-    W >>= 1;
-    lds = TL::lds_doubles(W) * sizeof(double);
-  }
-  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "image too large for LDS");
-  if (const char* pad = std::getenv("RHMC_LDS_MIN")) {  // experiment: cap workgroups per CU
-    const size_t want = (size_t)std::atol(pad);
-    if (want > lds && want <= (size_t)ctx->max_lds) lds = want;
-  }
-  const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
-  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_k1_tiledw<IMG, LPC, PROF>), grid, block, lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
-}
 
 // Register-window single-star kernel (rhmc_tiledr.hpp).
 template <int IMG, int WIN, typename DT, bool PROF>
@@ -1042,29 +945,25 @@ int launch_tiledr_t(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
   constexpr int W = 4;
   const int64_t waves = (a.n_chains + TL::CPW - 1) / TL::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  // RHMC_LDS_MIN pads the LDS request (experiment: 82 KB = one workgroup per
-  // CU; at C2 the dispatcher already spreads the 256 workgroups one per CU:
-  // 1.2255 vs 1.2251 ms per launch, measured).
-  if (const char* pad = std::getenv("RHMC_LDS_MIN")) {
-    const size_t want = (size_t)std::atol(pad);
-    if (want <= (size_t)ctx->max_lds && want >= TL::lds_bytes()) lds = want;
-  }
   hipLaunchKernelGGL((leapfrog_k1_tiledr<IMG, WIN, DT, PROF>), grid, block, lds, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
 // Register-window kernel (rhmc_tiledr.hpp): the 28-pixel window when the PSF
-// allows it (RHMC_KERNEL=tiledr32 forces 32), the fp32 pixel cache when the
-// image allows it exactly (RHMC_KERNEL=tiledr64 forces fp64).
+// allows it (RHMC_KERNEL_REGWIN32 forces 32), the fp32 pixel cache when the
+// image allows it exactly (RHMC_KERNEL_REGWIN_F64 forces fp64).  A library
+// built with -DRHMC_PHASE_PROF (make prof, tools/phase_prof.py only) runs the
+// phase-timing instantiation instead, which writes cycle counts over the state.
 template <int IMG>
 int launch_tiledr(const rhmc_ctx* ctx, LeapArgsK1 a, hipStream_t s) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  const bool w28 = reg_window_ok(28, a.c.inv_two_sig2) && !(e && std::strcmp(e, "tiledr32") == 0);
-  const bool f32 = ctx->img_f32 && !(e && std::strcmp(e, "tiledr64") == 0);
-  if (e && std::strcmp(e, "profr") == 0 && w28 && f32) {
+  const bool w28 = reg_window_ok(28, a.c.inv_two_sig2) && ctx->kernel != RHMC_KERNEL_REGWIN32;
+  const bool f32 = ctx->img_f32 && ctx->kernel != RHMC_KERNEL_REGWIN_F64;
+#ifdef RHMC_PHASE_PROF
+  if (w28 && f32) {
     a.Df = ctx->d_Df;
     return launch_tiledr_t<IMG, 28, float, true>(ctx, a, s);
   }
+#endif
   if (f32) {
     a.Df = ctx->d_Df;
     return w28 ? launch_tiledr_t<IMG, 28, float, false>(ctx, a, s)
@@ -1097,36 +996,27 @@ int launch_tiledl_lpc(const rhmc_ctx* ctx, LeapArgsK1 a, bool f32, hipStream_t s
 }
 
 // Lanes per chain of the lane-group kernel for a K = 1 batch of n chains, or 0
-// for the register-window kernel.  RHMC_KERNEL=tiledl1 / tiledl4 force it
-// (suffix _64: fp64 image in LDS); any other forced kernel turns it off.
+// for the register-window kernel.  RHMC_KERNEL_LANE1 / _LANE4 / _LANE1_F64
+// force it, RHMC_KERNEL_REGWIN* turn it off.
 // Measured (C2 geometry, 500 steps, chain-steps/s): 16384 chains tiledr
 // 1.99e9 / LPC 4 2.25e9; 65536: 2.28e9 / LPC 1 3.06e9; 131072: 2.31e9 / 3.59e9.
 constexpr int64_t kLaneChains1 = 65536;   // >= one 64-chain wave per SIMD
 constexpr int64_t kLaneChains4 = 16384;   // >= one 16-chain wave per SIMD
-int tiledl_lpc(int64_t n, const char* e) {
-  if (e && std::strncmp(e, "tiledl", 6) == 0) return e[6] == '4' ? 4 : 1;
-  if (e) return 0;
+int tiledl_lpc(int64_t n, int kern) {
+  if (kern == RHMC_KERNEL_LANE1 || kern == RHMC_KERNEL_LANE1_F64) return 1;
+  if (kern == RHMC_KERNEL_LANE4) return 4;
+  if (kern == RHMC_KERNEL_REGWIN || kern == RHMC_KERNEL_REGWIN32 || kern == RHMC_KERNEL_REGWIN_F64)
+    return 0;
   return n >= kLaneChains1 ? 1 : n >= kLaneChains4 ? 4 : 0;
 }
 
 template <int IMG>
 int launch_tiledl(const rhmc_ctx* ctx, const LeapArgsK1& a, int lpc, hipStream_t s) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  const bool f32 = ctx->img_f32 && !(e && std::strstr(e, "_64"));
+  const bool f32 = ctx->img_f32 && ctx->kernel != RHMC_KERNEL_LANE1_F64;
   return lpc == 4 ? launch_tiledl_lpc<IMG, 4>(ctx, a, f32, s)
                   : launch_tiledl_lpc<IMG, 1>(ctx, a, f32, s);
 }
 
-// Windowed single-star kernels: register-window (default, RHMC_KERNEL=tiledr)
-// or the LDS-operand kernel with 16 / 32 lanes per chain (tiledw / tiledw32).
-template <int IMG>
-int launch_tiledw(const rhmc_ctx* ctx, const LeapArgsK1& a, hipStream_t s) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  if (e && std::strcmp(e, "tiledw32") == 0) return launch_tiledw_lpc<IMG, 32>(ctx, a, s);
-  if (e && std::strcmp(e, "profw16") == 0) return launch_tiledw_lpc<IMG, 16, true>(ctx, a, s);
-  if (e && std::strcmp(e, "profw32") == 0) return launch_tiledw_lpc<IMG, 32, true>(ctx, a, s);
-  return launch_tiledw_lpc<IMG, 16>(ctx, a, s);
-}
 
 // V (and optionally T) of n chains on device buffers, async on `s`.
 template <int IMG>
@@ -1151,10 +1041,10 @@ int launch_energy_k1(const rhmc_ctx* ctx, EnergyK1Args k, hipStream_t s) {
 int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const double* d_p,
                   double* d_V, double* d_T, int64_t n, int K, int f_pos, hipStream_t s) {
   // one star on a 32/48/64-px image: the register-window energy kernel
-  // (rhmc_mhk1.hpp); any RHMC_KERNEL override keeps the per-wave kernels
+  // (rhmc_mhk1.hpp); RHMC_KERNEL_GENERIC / _WINDOWED keep the per-wave kernels
   const int side = ctx->rows;
   if (K == 1 && !c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
-      reg_window_ok(28, c.inv_two_sig2) && !std::getenv("RHMC_KERNEL")) {
+      reg_window_ok(28, c.inv_two_sig2) && !per_wave_forced(ctx)) {
     if (n == 0) return RHMC_OK;
     EnergyK1Args k;
     k.q = d_q;
@@ -1202,27 +1092,6 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   return dispatch_k<EnergyLaunch>(K, grid, block, lds, s, a);
 }
 
-template <int IMG, int KMAX>
-int launch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
-  using TK = TiledK<IMG, KMAX>;
-  int W = 4;
-  while (W > 1 && TK::lds_doubles(W) * sizeof(double) > (size_t)ctx->max_lds) W >>= 1;
-  const size_t lds = TK::lds_doubles(W) * sizeof(double);
-  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "tiledk LDS");
-  const dim3 grid((unsigned)((a.n_chains + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_tiledk_kernel<IMG, KMAX>), grid, block, lds, s, a);
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
-}
-
-template <int IMG>
-int dispatch_tiledk(const rhmc_ctx* ctx, const LeapArgs& a, hipStream_t s) {
-  if (a.K <= 2) return launch_tiledk<IMG, 2>(ctx, a, s);
-  if (a.K <= 4) return launch_tiledk<IMG, 4>(ctx, a, s);
-  if (a.K <= 8) return launch_tiledk<IMG, 8>(ctx, a, s);
-  if (a.K <= 10) return launch_tiledk<IMG, 10>(ctx, a, s);
-  return launch_tiledk<IMG, 16>(ctx, a, s);
-}
 
 // Multi-star register-window kernel (rhmc_tiledrk.hpp): K in [2, 64], square
 // image of side >= 32, PSF narrow enough for the 28-row window.
@@ -1234,13 +1103,9 @@ bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c) {
 // Which multi-star kernel serves (K, image) by default: the register-window
 // kernel wherever it applies (C3 with LDS factor tables: 18.0 ms per 100 steps
 // against 20.3 for the full-image tiled kernel; C5: 3.2x the windowed kernel).
-// RHMC_KERNEL=tiledk / windowed / generic force the older families.
+// RHMC_KERNEL_GENERIC / _WINDOWED force the one-wave-per-chain families.
 bool use_tiledrk(const rhmc_ctx* ctx, int K, const Consts& c) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  if (e && (std::strcmp(e, "tiledk") == 0 || std::strcmp(e, "windowed") == 0 ||
-            std::strcmp(e, "generic") == 0))
-    return false;
-  return tiledrk_ok(ctx, K, c);
+  return !per_wave_forced(ctx) && tiledrk_ok(ctx, K, c);
 }
 
 template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
@@ -1258,12 +1123,10 @@ int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_t
 }
 
 // Factor tables in LDS (TiledRK<..., TAB>) for images up to 64 px with K <= 16,
-// where every window overlaps (nearly) every star; RHMC_KERNEL=tiledrk_notab
+// where every window overlaps (nearly) every star; RHMC_KERNEL_MULTIWIN_NOTAB
 // forces the exp path there.
 bool kr_tables(const rhmc_ctx* ctx, int K) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  if (e && std::strcmp(e, "tiledrk_notab") == 0) return false;
-  return ctx->rows <= 64 && K <= 16;
+  return ctx->kernel != RHMC_KERNEL_MULTIWIN_NOTAB && ctx->rows <= 64 && K <= 16;
 }
 
 template <int SOLVER = RHMC_SOLVER_IMPLICIT>
@@ -1282,11 +1145,13 @@ int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, int f_pos, hipStream_t s) {
 
 // Pixel-major multi-star kernel (rhmc_pixk.hpp): the default for 2 <= K <= 10
 // on a 32/48-px fp32-exact image (C3: 1.23e8 chain-steps/s against 1.05e8 for
-// the window-major kernel with LDS tables, measured A/B on one box).  Any other
-// RHMC_KERNEL value keeps the older kernels.
+// the window-major kernel with LDS tables, measured A/B on one box).
+// RHMC_KERNEL_MULTIWIN* force the window-major kernel, GENERIC / WINDOWED the
+// per-wave ones.
 bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
-  const char* e = std::getenv("RHMC_KERNEL");
-  const bool want = !e || std::strcmp(e, "pixk") == 0;
+  const int k = ctx->kernel;
+  const bool want = !per_wave_forced(ctx) && k != RHMC_KERNEL_MULTIWIN &&
+                    k != RHMC_KERNEL_MULTIWIN_NOTAB;
   return want && K >= 2 && K <= 10 && !c.use_Vc && ctx->img_f32 && ctx->rows == ctx->cols &&
          (ctx->rows == 32 || ctx->rows == 48);
 }
@@ -1323,19 +1188,12 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   if (n_chains == 0) return RHMC_OK;
   HIP_TRY(hipSetDevice(ctx->device));
   const int side = ctx->rows;
-  const char* kenv = std::getenv("RHMC_KERNEL");
-  const bool kr_k1 = K == 1 && kenv && std::strncmp(kenv, "tiledrk", 7) == 0;  // experiment
-  const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_generic() &&
-                  !force_windowed() && !kr_k1;
-  const char* ke = std::getenv("RHMC_KERNEL");
+  // one star: the register-window kernel (C1, C2) or, from 16 Ki chains, the
+  // lane-group kernel (C4 shards); wider PSFs and other image sides take the
+  // generic kernel below
+  const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !per_wave_forced(ctx);
   const bool img_ok = side == 32 || side == 48 || side == 64 || side == 96 || side == 128;
-  // register-window kernel (default) / LDS-operand window kernel (tiledw*)
-  const bool k1r = k1 && img_ok && !force_full_image_k1() && reg_window_ok(32, a.c.inv_two_sig2) &&
-                   !(ke && std::strncmp(ke, "tiledw", 6) == 0) &&
-                   !(ke && std::strncmp(ke, "profw", 5) == 0);
-  const bool k1w = !k1r && k1 && window_exact(a.c) && !force_full_image_k1() &&
-                   (side == 48 || side == 64 || side == 96 || side == 128);
-  if (k1r || k1w || (k1 && (side == 16 || side == 32 || side == 48 || side == 64))) {
+  if (k1 && img_ok && reg_window_ok(32, a.c.inv_two_sig2)) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -1349,36 +1207,20 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     t.pad = 0;
     t.Df = nullptr;
     t.c = a.c;
-    if (k1r) {
-      const int lpc = tiledl_lpc(n_chains, ke);
-      if (lpc && side <= 64 && reg_window_ok(28, a.c.inv_two_sig2)) {
-        switch (side) {
-          case 32: return launch_tiledl<32>(ctx, t, lpc, s);
-          case 48: return launch_tiledl<48>(ctx, t, lpc, s);
-          default: return launch_tiledl<64>(ctx, t, lpc, s);
-        }
-      }
+    const int lpc = tiledl_lpc(n_chains, ctx->kernel);
+    if (lpc && side <= 64 && reg_window_ok(28, a.c.inv_two_sig2)) {
       switch (side) {
-        case 32: return launch_tiledr<32>(ctx, t, s);
-        case 48: return launch_tiledr<48>(ctx, t, s);
-        case 64: return launch_tiledr<64>(ctx, t, s);
-        case 96: return launch_tiledr<96>(ctx, t, s);
-        default: return launch_tiledr<128>(ctx, t, s);
-      }
-    }
-    if (k1w) {
-      switch (side) {
-        case 48: return launch_tiledw<48>(ctx, t, s);
-        case 64: return launch_tiledw<64>(ctx, t, s);
-        case 96: return launch_tiledw<96>(ctx, t, s);
-        default: return launch_tiledw<128>(ctx, t, s);
+        case 32: return launch_tiledl<32>(ctx, t, lpc, s);
+        case 48: return launch_tiledl<48>(ctx, t, lpc, s);
+        default: return launch_tiledl<64>(ctx, t, lpc, s);
       }
     }
     switch (side) {
-      case 16: return launch_tiled<16>(ctx, t, s);
-      case 32: return launch_tiled<32>(ctx, t, s);
-      case 48: return launch_tiled<48>(ctx, t, s);
-      default: return launch_tiled<64>(ctx, t, s);
+      case 32: return launch_tiledr<32>(ctx, t, s);
+      case 48: return launch_tiledr<48>(ctx, t, s);
+      case 64: return launch_tiledr<64>(ctx, t, s);
+      case 96: return launch_tiledr<96>(ctx, t, s);
+      default: return launch_tiledr<128>(ctx, t, s);
     }
   }
   if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
@@ -1427,8 +1269,6 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   a.n_chains = n_chains;
   a.K = K;
   a.n_steps = n_steps;
-  if (K >= 2 && K <= kMaxKGeneric && !force_generic() && (side == 32 || side == 48))
-    return side == 32 ? dispatch_tiledk<32>(ctx, a, s) : dispatch_tiledk<48>(ctx, a, s);
   if ((rc = pick_waves(ctx, K, &lds, &W))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   return dispatch_k<LeapLaunch>(K, grid, block, lds, s, a);
@@ -1440,14 +1280,14 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
 
 // One star where launch_leapfrog takes the register-window kernel (28-px
 // window, 32/48/64-px image, fewer chains than the lane-group threshold): the
-// whole MH loop in one launch (rhmc_mhk1.hpp).  RHMC_MH=unfused, or any
-// RHMC_KERNEL override, keeps the four-kernel loop below.
+// whole MH loop in one launch (rhmc_mhk1.hpp).  RHMC_OPT_MH_FUSED = 0, or a
+// forced kernel other than REGWIN, keeps the four-kernel loop below.
 bool mh_k1_fused(const rhmc_ctx* ctx, const Consts& c, int64_t n) {
-  const char* m = std::getenv("RHMC_MH");
-  if ((m && std::strcmp(m, "unfused") == 0) || std::getenv("RHMC_KERNEL")) return false;
+  if (!ctx->mh_fused) return false;
+  if (ctx->kernel != RHMC_KERNEL_AUTO && ctx->kernel != RHMC_KERNEL_REGWIN) return false;
   const int side = ctx->rows;
   return !c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
-         reg_window_ok(28, c.inv_two_sig2) && tiledl_lpc(n, nullptr) == 0;
+         reg_window_ok(28, c.inv_two_sig2) && tiledl_lpc(n, ctx->kernel) == 0;
 }
 
 template <int IMG>
@@ -1596,10 +1436,10 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   if (rc) return rc;
   if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
   if (n == 0) return RHMC_OK;
-  // one star on a 32/48/64-px image: register-window kernel (RHMC_KERNEL=windowed
-  // keeps the windowed one)
+  // one star on a 32/48/64-px image: register-window kernel (RHMC_KERNEL_GENERIC
+  // / _WINDOWED keep the windowed one)
   const int side = ctx->rows;
-  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !force_windowed() &&
+  if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !per_wave_forced(ctx) &&
       (side == 32 || side == 48 || side == 64) && reg_window_ok(28, a.c.inv_two_sig2)) {
     LeapArgsK1 t;
     t.q = d_q;
@@ -1707,11 +1547,11 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   if (rc) return rc;
   if (n == 0) return RHMC_OK;
   if (!d_dt || !d_steps) return fail(RHMC_ERR_ARG, "dt/steps is NULL");
-  // one star on a 32/48/64-px image: register-window kernel (any RHMC_KERNEL
-  // override keeps the windowed one)
+  // one star on a 32/48/64-px image: register-window kernel (RHMC_KERNEL_GENERIC
+  // / _WINDOWED keep the windowed one)
   const int side = ctx->rows;
   if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
-      reg_window_ok(28, a.c.inv_two_sig2) && !std::getenv("RHMC_KERNEL")) {
+      reg_window_ok(28, a.c.inv_two_sig2) && !per_wave_forced(ctx)) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -1733,11 +1573,9 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
     }
   }
   // many stars: the pixel-major kernel (full image, any PSF width) or the
-  // multi-star register-window kernel (rhmc_tiledrk.hpp); RHMC_KERNEL=tiledrk
-  // forces the latter, any other override keeps the windowed kernel below.
-  const char* ke = std::getenv("RHMC_KERNEL");
-  const bool kr = use_tiledrk(ctx, K, a.c) && (!ke || std::strncmp(ke, "tiledrk", 7) == 0);
-  if (use_pixk(ctx, K, a.c) || kr) {
+  // multi-star register-window kernel (rhmc_tiledrk.hpp); RHMC_KERNEL_MULTIWIN
+  // forces the latter, GENERIC / WINDOWED the windowed kernel below.
+  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -1917,6 +1755,32 @@ int rhmc_ctx_create(int device, const double* D, int32_t rows, int32_t cols, rhm
   }
   *out = ctx;
   return RHMC_OK;
+}
+
+int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  switch (option) {
+    case RHMC_OPT_KERNEL:
+      if (value < RHMC_KERNEL_AUTO || value > RHMC_KERNEL_MULTIWIN_NOTAB)
+        return fail(RHMC_ERR_ARG, "unknown RHMC_KERNEL_* value " + std::to_string(value));
+      ctx->kernel = value;
+      return RHMC_OK;
+    case RHMC_OPT_MH_FUSED:
+      if (value != 0 && value != 1) return fail(RHMC_ERR_ARG, "RHMC_OPT_MH_FUSED must be 0 or 1");
+      ctx->mh_fused = value;
+      return RHMC_OK;
+    default:
+      return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
+  }
+}
+
+int rhmc_ctx_get_option(rhmc_ctx* ctx, int32_t option, int32_t* value) {
+  if (!ctx || !value) return fail(RHMC_ERR_ARG, "NULL argument");
+  switch (option) {
+    case RHMC_OPT_KERNEL: *value = ctx->kernel; return RHMC_OK;
+    case RHMC_OPT_MH_FUSED: *value = ctx->mh_fused; return RHMC_OK;
+    default: return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
+  }
 }
 
 int rhmc_ctx_image_device(rhmc_ctx* ctx, const double** d_image) {

@@ -34,7 +34,6 @@
 #pragma once
 #include "rhmc_exp.hpp"
 #include "rhmc_k1step.hpp"
-#include "rhmc_tiled.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_wave.hpp"
 

@@ -35,8 +35,6 @@
 #pragma once
 #include "rhmc_exp.hpp"
 #include "rhmc_k1step.hpp"
-#include "rhmc_tiled.hpp"
-#include "rhmc_tiled2.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 

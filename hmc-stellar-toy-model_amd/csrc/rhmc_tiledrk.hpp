@@ -33,8 +33,6 @@
 #pragma once
 #include "rhmc_exp.hpp"
 #include "rhmc_k1step.hpp"
-#include "rhmc_tiled.hpp"
-#include "rhmc_tiled2.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_wave.hpp"
 
@@ -433,8 +431,20 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) fm[t] = flux_metric(f[t], c, lc);
   kr_publish<SLOTS>(tab, f, x, y, own);
+  unsigned long long near_bal = 0ull;
   for (int s = 0;; ++s) {
     double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+    if (s > 0) {
+      // near-wall test of this iteration's position reflections (below; x, y
+      // are unchanged until the next q-loop), kept as a wave-uniform ballot
+      // mask in SGPRs: these loops run at the VGPR limit
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const bool nx = (x[t] < 0.0 || x[t] > edge) && near_edge(x[t], edge);
+        const bool ny = (y[t] < 0.0 || y[t] > edge) && near_edge(y[t], edge);
+        near_bal |= __builtin_amdgcn_ballot_w64(own[t] && (nx || ny));
+      }
+    }
     grad(x, y, gf, gx, gy);
     if constexpr (RELOAD) kr_reload<SLOTS>(tab, f, x, y, own);
     // Recompute the flux metric instead of keeping it live through the
@@ -456,6 +466,7 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
         if (f[t] < c.f_lim) {                      // :554-564
           pf[t] = -pf[t];
           if (own[t]) st |= RHMC_STATUS_REFLECT_F;
+          if (own[t] && f[t] >= c.near_f) st |= RHMC_STATUS_NEAR_WALL;
         }
         if (x[t] < 0.0 || x[t] > edge) {
           px[t] = -px[t];
@@ -548,6 +559,8 @@ __device__ __forceinline__ void km_steps(double (&f)[SLOTS], double (&x)[SLOTS],
     }
     kr_publish<SLOTS>(tab, f, x, y, own);
   }
+  // the chain's 32-lane half of the near-wall mask
+  if ((near_bal >> (lane_id() & 32)) & 0xFFFFFFFFull) st |= RHMC_STATUS_NEAR_WALL;
 }
 
 // n_steps steps of single_gym's explicit integrators for

@@ -24,12 +24,23 @@ struct Consts {
   // reciprocals for the division-lean forms, computed once on the host (a
   // device-side computation gets re-materialised inside the step loop)
   double inv_gff2, inv_g1, Bg2, inv_gxx, inv_two_sig2, inv_norm, inv_var;
+  double two_Bg2;  // 2 B/g2 (exact), a kernel argument so it stays in SGPRs
   // PSF factor recurrences (rhmc_tiledr.hpp factors): ratio of successive row
   // ratios exp(-2/(2 sigma^2)), of column ratios 4 apart exp(-32/(2 sigma^2)),
   // and the largest |window offset| for which the recurrence stays in range
   double k_row, k_col4, rec_vmax;
+  // near-wall threshold of the flux wall: f_lim - 2^-40 max(1, |f_lim|)
+  double near_f;
   int counter_max, use_prior, use_Vc, pad;
 };
+
+// A position reflection (v < 0 or v > edge, sampler_RHMC.py:561-564) whose
+// coordinate lies within 2^-40 (9.1e-13) of its wall, relative to max(1, wall)
+// (edge >= 1): RHMC_STATUS_NEAR_WALL.  Only meaningful when v
+// reflected.  Powers of two keep the constants inline literals (no registers).
+__device__ __forceinline__ bool near_edge(double v, double edge) {
+  return v >= -0x1p-40 && (v - edge) <= edge * 0x1p-40;
+}
 
 // ---------------------------------------------------------------- lane moves
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
@@ -112,7 +123,7 @@ __device__ __forceinline__ double rcp_nr(double d) {  // ~correctly rounded 1/d
 }
 
 struct LeanConsts {
-  double inv_gff2, c0, inv_g1, Bg2, inv_gxx, f_low;
+  double inv_gff2, c0, inv_g1, Bg2, two_Bg2, inv_gxx, f_low;
   double inv_two_sig2, inv_norm, inv_var;  // PSF exponent / normalisation, 1/var
   double k_row, k_col4, rec_vmax;          // PSF factor recurrences (Consts)
 };
@@ -123,6 +134,7 @@ __device__ __forceinline__ LeanConsts lean_consts(const Consts& c) {
   l.c0 = c.c0;
   l.inv_g1 = c.inv_g1;
   l.Bg2 = c.Bg2;
+  l.two_Bg2 = c.two_Bg2;
   l.inv_gxx = c.inv_gxx;
   l.f_low = c.f_low;
   l.inv_two_sig2 = c.inv_two_sig2;
@@ -277,6 +289,61 @@ __device__ __forceinline__ double metric_flux_term(double f, const Consts& c) {
 __device__ __forceinline__ double dtaudq_coef(double f, const Consts& c) {
   const double h = H_ff(f, c);
   return -H_ff_grad(f, c) / (h * h);
+}
+
+// ------------------------------------------------------- DPP / permlane sums
+template <int CTRL>
+__device__ __forceinline__ double dpp_move(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// gfx950 v_permlane{16,32}_swap on both 32-bit halves of a double, called
+// with the same register as both operands: returns (a, b) such that a + b
+// adds row r to row r^1 (16) or half h to half h^1 (32), with the SAME
+// operand order in both partner rows.
+template <bool SWAP32>
+__device__ __forceinline__ double swap_add(double v) {
+  const long long bits = __double_as_longlong(v);
+  const unsigned lo = (unsigned)bits, hi = (unsigned)(bits >> 32);
+  unsigned a_lo, b_lo, a_hi, b_hi;
+  if (SWAP32) {
+    const auto l = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a_lo = l[0]; b_lo = l[1]; a_hi = h[0]; b_hi = h[1];
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    a_lo = l[0]; b_lo = l[1]; a_hi = h[0]; b_hi = h[1];
+  }
+  const double a = __longlong_as_double(((long long)a_hi << 32) | a_lo);
+  const double b = __longlong_as_double(((long long)b_hi << 32) | b_lo);
+  return a + b;
+}
+
+// All-reduce over the wave: xor-1 / xor-2 quad permutes, half-mirror and
+// mirror inside each 16-lane row (partners add the same two values, so every
+// lane of a row holds the same bits), then row pairs and half pairs by the
+// permlane swaps.  Deterministic and bit-identical in every lane.
+__device__ __forceinline__ double wave_sum_dpp(double v) {
+  v += dpp_move<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_move<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_move<0x141>(v);  // row_half_mirror
+  v += dpp_move<0x140>(v);  // row_mirror
+  v = swap_add<false>(v);   // rows 0+1, 2+3
+  return swap_add<true>(v); // (0+1) + (2+3)
+}
+
+// Sum over the 32 lanes of each half-wave; every lane of a half gets its
+// half's sum (rows 0+1 and rows 2+3), bit-identical within the half.
+__device__ __forceinline__ double half_sum_dpp(double v) {
+  v += dpp_move<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_move<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_move<0x141>(v);  // row_half_mirror
+  v += dpp_move<0x140>(v);  // row_mirror
+  return swap_add<false>(v);
 }
 
 }  // namespace rhmc

@@ -17,7 +17,6 @@
 // D stays in global memory (512 KB at 256x256, L2-resident and shared by all
 // chains).  Per-wave LDS: windowed PSF factor tables, 2 x K x 33 doubles.
 #pragma once
-#include "rhmc_tiled.hpp"
 #include "rhmc_wave.hpp"
 
 namespace rhmc {

@@ -26,10 +26,24 @@ STATUS_PLOOP_CAP = 2
 STATUS_QLOOP_CAP = 4
 STATUS_REFLECT_F = 8
 STATUS_REFLECT_XY = 16
+STATUS_NEAR_WALL = 32     # a reflection within 1e-12 of its wall
+
+OPT_KERNEL = 1            # rhmc_ctx_set_option (include/rhmc.h)
+OPT_MH_FUSED = 2
+# RHMC_KERNEL_* values by name
+KERNELS = {"auto": 0, "generic": 1, "windowed": 2, "regwin": 3, "regwin32": 4,
+           "regwin_f64": 5, "lane1": 6, "lane4": 7, "lane1_f64": 8, "pixmajor": 9,
+           "multiwin": 10, "multiwin_notab": 11}
+# What a new Context selects unless told otherwise.  Production code leaves
+# these alone; the parity tests set them (monkeypatch) to run the same inputs
+# through every kernel family.  The library itself reads no environment.
+DEFAULT_KERNEL = "auto"
+DEFAULT_MH_FUSED = True
 
 EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
-           "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_leapfrog",
+           "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_ctx_set_option",
+           "rhmc_ctx_get_option", "rhmc_leapfrog",
            "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
            "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
            "rhmc_gen_image", "rhmc_gen_image_device", "rhmc_hmc_random",
@@ -94,6 +108,8 @@ def _load():
         "rhmc_ctx_image_device": (ctypes.c_int, [vp, P(vp)]),
         "rhmc_ctx_destroy": (None, [vp]),
         "rhmc_ctx_synchronize": (ctypes.c_int, [vp]),
+        "rhmc_ctx_set_option": (ctypes.c_int, [vp, ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_ctx_get_option": (ctypes.c_int, [vp, ctypes.c_int32, P(ctypes.c_int32)]),
         "rhmc_leapfrog": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, ctypes.c_int64,
                                          ctypes.c_int32, ctypes.c_int32, c_ip, c_ip]),
         "rhmc_leapfrog_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, ctypes.c_int64,
@@ -186,9 +202,11 @@ def make_params(dt, delta, counter_max, B_count, f_lim, f_low, fwhm_pix, g_xx, g
 class Context:
     """One GPU + one data image (rhmc_ctx)."""
 
-    def __init__(self, D, device=0):
+    def __init__(self, D, device=0, kernel=None, mh_fused=None):
         """D: the data image, or None for a context whose image comes from
-        gen_image(..., install=True)."""
+        gen_image(..., install=True).  kernel: a KERNELS name (default
+        DEFAULT_KERNEL), mh_fused: one-launch MH where available (default
+        DEFAULT_MH_FUSED)."""
         h = ctypes.c_void_p()
         if D is None:
             _check(_lib.rhmc_ctx_create(int(device), None, 0, 0, ctypes.byref(h)))
@@ -202,6 +220,23 @@ class Context:
             self.shape = D.shape
         self._h = h
         self.device = device
+        self.set_kernel(DEFAULT_KERNEL if kernel is None else kernel)
+        self.set_option(OPT_MH_FUSED, int(bool(DEFAULT_MH_FUSED if mh_fused is None
+                                               else mh_fused)))
+
+    def set_option(self, option, value):
+        _check(_lib.rhmc_ctx_set_option(self._h, int(option), int(value)))
+
+    def get_option(self, option):
+        v = ctypes.c_int32()
+        _check(_lib.rhmc_ctx_get_option(self._h, int(option), ctypes.byref(v)))
+        return v.value
+
+    def set_kernel(self, name):
+        """Kernel family for this context's compute calls (KERNELS name)."""
+        if name not in KERNELS:
+            raise ValueError("unknown kernel %r (one of %s)" % (name, ", ".join(KERNELS)))
+        self.set_option(OPT_KERNEL, KERNELS[name])
 
     @property
     def handle(self):

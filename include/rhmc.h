@@ -65,7 +65,7 @@
 extern "C" {
 #endif
 
-#define RHMC_ABI_VERSION 1
+#define RHMC_ABI_VERSION 2
 
 enum {
   RHMC_OK = 0,
@@ -89,6 +89,11 @@ enum {
 #define RHMC_STATUS_QLOOP_CAP   4u  /* q fixed-point loop stopped at counter_max */
 #define RHMC_STATUS_REFLECT_F   8u  /* flux-wall reflection (:558-559)           */
 #define RHMC_STATUS_REFLECT_XY 16u  /* edge reflection (:561-564)                */
+/* A reflection of the implicit step fired with its coordinate within 2^-40 (9.1e-13) of
+ * the wall (relative to max(1, |wall|): f_lim, 0 or R-1; :554-564).  Such a
+ * chain can legitimately reflect the other way on a last-bit difference
+ * (SURVEY §8(c)), so callers report these chains separately. */
+#define RHMC_STATUS_NEAR_WALL  32u
 
 /* Instance state read by the step (POD; all fp64 except the flags). */
 typedef struct rhmc_params {
@@ -111,6 +116,52 @@ typedef struct rhmc_params {
 } rhmc_params;
 
 typedef struct rhmc_ctx rhmc_ctx;
+
+/*
+ * Context options (rhmc_ctx_set_option).  Nothing in the library reads the
+ * environment: kernel selection is per context, AUTO unless a caller (the
+ * parity tests) sets it.
+ *
+ * RHMC_OPT_KERNEL: the kernel family the compute calls use.  A family that
+ * does not serve the call's configuration (K, image side, PSF width, fp32
+ * exactness of the image) leaves the automatic choice for that call.
+ *   AUTO            the default dispatch
+ *   GENERIC         one wave per chain, image in LDS (K <= 16, image + tables
+ *                   fit LDS; else WINDOWED); explicit integrators and
+ *                   HMC_random take WINDOWED; MH runs the four-kernel loop
+ *   WINDOWED        one wave per chain, 32-px star windows, image in HBM/L2
+ *   REGWIN          K = 1 register-window kernel at every batch size
+ *   REGWIN32        ... forced onto the 32-px window
+ *   REGWIN_F64      ... with an fp64 pixel cache
+ *   LANE1 / LANE4   K = 1 lane-group kernel, 1 / 4 lanes per chain, at every
+ *                   batch size; LANE1_F64: fp64 image in LDS
+ *   PIXMAJOR        2 <= K <= 10 pixel-major kernel (the AUTO choice there)
+ *   MULTIWIN        K >= 2 multi-star register-window kernel (also where the
+ *                   pixel-major kernel would serve); MULTIWIN_NOTAB without
+ *                   the LDS factor tables
+ * RHMC_OPT_MH_FUSED: 1 (default) = one-launch MH where a fused kernel exists,
+ *   0 = the four-kernel loop (begin / leapfrog / energy / end) always.
+ */
+enum {
+  RHMC_OPT_KERNEL = 1,
+  RHMC_OPT_MH_FUSED = 2
+};
+enum {
+  RHMC_KERNEL_AUTO = 0,
+  RHMC_KERNEL_GENERIC = 1,
+  RHMC_KERNEL_WINDOWED = 2,
+  RHMC_KERNEL_REGWIN = 3,
+  RHMC_KERNEL_REGWIN32 = 4,
+  RHMC_KERNEL_REGWIN_F64 = 5,
+  RHMC_KERNEL_LANE1 = 6,
+  RHMC_KERNEL_LANE4 = 7,
+  RHMC_KERNEL_LANE1_F64 = 8,
+  RHMC_KERNEL_PIXMAJOR = 9,
+  RHMC_KERNEL_MULTIWIN = 10,
+  RHMC_KERNEL_MULTIWIN_NOTAB = 11
+};
+int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value);
+int rhmc_ctx_get_option(rhmc_ctx* ctx, int32_t option, int32_t* value);
 
 /* ABI version of the loaded library (== RHMC_ABI_VERSION when in sync). */
 int rhmc_abi_version(void);

@@ -1,7 +1,7 @@
 #!/bin/bash
-# One GPU session: smoke, parity tests, bench, rocprofv3 kernel trace.
-# Each GPU step has its own time limit; stop at the first crash/timeout
-# (rc >= 2 other than pytest's "tests failed" = 1).
+# One GPU session: smoke, parity tests, bench (N=1 and a 2-rank rehearsal on
+# the one GPU), rocprofv3 kernel trace.  Each GPU step has its own time limit;
+# stop at the first crash/timeout (rc >= 2 other than pytest's "tests failed").
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -17,10 +17,11 @@ step() {
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = test ]; then
   step 300 smoke python3 -c "import __graft_entry__ as g; g.smoke()"
-  step 900 pytest_gpu python3 -m pytest tests -m gpu -q -rf
+  step 1000 pytest_gpu python3 -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
   step 600 bench python3 bench.py
+  step 300 bench_2ranks env RHMC_BENCH_DEVICE=0 python3 bench.py --gpus 2 --no-cpu --steps 10
   step 600 rocprof rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu
 fi
 echo done

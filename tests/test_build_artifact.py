@@ -38,10 +38,14 @@ def _disassemble(tmp_path):
 def test_gfx950_code_object_present_and_hot_kernels_spill_free(tmp_path):
     funcs = _disassemble(tmp_path)
     leap = [f for f in funcs if "leapfrog" in f or "integrate_k1" in f]
-    assert any("leapfrog_k1_tiled" in f for f in leap)
+    assert any("leapfrog_k1_tiledr" in f for f in leap)
+    assert any("leapfrog_k1_tiledl" in f for f in leap)
+    assert any("leapfrog_pk" in f for f in leap) and any("leapfrog_kr" in f for f in leap)
     assert sum("integrate_k1_tiledr" in f for f in leap) == 18   # 3 images x 2 DT x 3 solvers
-    assert any("leapfrog_tiledk_kernel" in f for f in leap)
     assert any("leapfrog_win_kernel" in f for f in leap)
+    # superseded families are gone (round 3)
+    assert not any("leapfrog_k1_tiled<" in f or "leapfrog_k1_tiled2" in f or
+                   "leapfrog_k1_tiledw" in f or "leapfrog_tiledk_kernel" in f for f in funcs)
     for name in leap:
         if "win_kernel" in name:
             continue        # windowed kernel: a few scratch words from exp/pow (measured, small)

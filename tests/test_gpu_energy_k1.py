@@ -1,6 +1,6 @@
 """The one-star register-window energy kernel (energy_k1_tiledr, rhmc_mhk1.hpp:
 V = image background + window correction, 16 lanes per chain) against the
-full-image per-wave energy kernels (any RHMC_KERNEL override selects them)
+full-image per-wave energy kernels (the "generic" / "windowed" kernel options select them)
 and the CPU oracle (RefModel.V / T, sampler_RHMC.py:294-363):
 
 * V and T to 1e-12 relative on a C2-sized batch, with chains inside the
@@ -34,12 +34,11 @@ def _batch(wl, n, side, rng):
 
 
 def _energies(ctx, P, q, p, monkeypatch, new, **kw):
-    if not new:
-        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+    ctx.set_kernel("auto" if new else "windowed")
     try:
         return ctx.energy(P, q, p, **kw)
     finally:
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
+        ctx.set_kernel("auto")
 
 
 def _close(a, b, rtol):

@@ -37,7 +37,6 @@ def _check(capi, D, par, q0, p0, steps, chains=None):
 
 
 def test_far_chain_wave_and_edges(gpu_lib, monkeypatch):
-    monkeypatch.delenv("RHMC_KERNEL", raising=False)
     wl = workloads.make("C2", n_chains=12)
     q0, p0 = wl.q0.copy(), wl.p0.copy()
     q0[2, 1], q0[2, 2] = 300.0, -250.0     # wave 0: far outside (direct factors)
@@ -50,7 +49,6 @@ def test_far_chain_wave_and_edges(gpu_lib, monkeypatch):
 
 @pytest.mark.parametrize("fwhm", [1.2, 2.5])
 def test_psf_widths_either_side_of_the_range_guard(gpu_lib, monkeypatch, fwhm):
-    monkeypatch.delenv("RHMC_KERNEL", raising=False)
     par, ftc = workloads.base_params(dt=0.1)
     par["fwhm_pix"] = fwhm
     rng = np.random.RandomState(int(fwhm * 10))

@@ -6,7 +6,7 @@ rhmc_integrate, at the bench's C2 geometry:
   hmc_step / rhmc_naive_step / rhmc_leapfrog_step (sampler_RHMC.py:628-645,
   :690-728) after 100 steps to 1e-9 (q) / 1e-8 (p) relative to |value| + 1,
   flux wall on (f_pos), with and without the flux prior;
-* the windowed kernel (RHMC_KERNEL=windowed, the other implementation of the
+* the windowed kernel (kernel option "windowed", the other implementation of the
   same step) agrees on the whole batch to the same tolerance;
 * batch invariance: a ragged subset run on its own is bit-identical;
 * a 32-px image (C1's) and a 64-px image take the same kernel family.
@@ -85,9 +85,11 @@ def test_c2_explicit_vs_oracle_and_windowed(c2, name, prior, monkeypatch):
                              return_status=True)
     assert not (st & capi.STATUS_NONFINITE).any()
     _check_sample(capi, wl, params, p0, name, q, p, (0, 1, 777, 2048, 2913, 4095))
-    monkeypatch.setenv("RHMC_KERNEL", "windowed")
-    qw, pw = ctx.integrate(P, _sid(capi, name), wl.q0, p0, N_STEPS, f_pos=True)
-    monkeypatch.delenv("RHMC_KERNEL")
+    ctx.set_kernel("windowed")
+    try:
+        qw, pw = ctx.integrate(P, _sid(capi, name), wl.q0, p0, N_STEPS, f_pos=True)
+    finally:
+        ctx.set_kernel("auto")
     err_q = np.abs(q - qw) / (np.abs(qw) + 1)
     err_p = np.abs(p - pw) / (np.abs(pw) + 1)
     assert err_q.max() <= 1e-9 and err_p.max() <= 1e-8, (err_q.max(), err_p.max())
@@ -173,9 +175,9 @@ def test_many_star_explicit_vs_oracle(gpu_lib, name, side, K, n_chains, monkeypa
         q, p, st = ctx.integrate(P, _sid(capi, name), wl.q0, p0, n, f_pos=True,
                                  return_status=True)
         assert not (st & capi.STATUS_NONFINITE).any()
-        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        ctx.set_kernel("windowed")
         qw, pw = ctx.integrate(P, _sid(capi, name), wl.q0, p0, n, f_pos=True)
-        monkeypatch.delenv("RHMC_KERNEL")
+        ctx.set_kernel("auto")
         idx = np.arange(min(n_chains, 13))
         qs, ps = ctx.integrate(P, _sid(capi, name), wl.q0[idx], p0[idx], n, f_pos=True)
     finally:

@@ -29,11 +29,11 @@ def _par(wl):
 
 
 def _run(capi, ctx, P, q0, p0, kernel, monkeypatch, steps=STEPS):
-    if kernel:
-        monkeypatch.setenv("RHMC_KERNEL", kernel)
-    else:
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
-    return ctx.leapfrog(P, q0, p0, steps, return_info=True)
+    ctx.set_kernel(kernel or "auto")
+    try:
+        return ctx.leapfrog(P, q0, p0, steps, return_info=True)
+    finally:
+        ctx.set_kernel("auto")
 
 
 @pytest.mark.parametrize("n", [16383, 16384, 65537])
@@ -43,7 +43,7 @@ def test_threshold_batches_match_register_window_and_oracle(gpu_lib, monkeypatch
     ctx = capi.Context(wl.D)
     P = capi.make_params(**wl.params)
     q, p, it, st = _run(capi, ctx, P, wl.q0, wl.p0, None, monkeypatch)       # default choice
-    qr, pr, itr, str_ = _run(capi, ctx, P, wl.q0, wl.p0, "tiledr", monkeypatch)
+    qr, pr, itr, str_ = _run(capi, ctx, P, wl.q0, wl.p0, "regwin", monkeypatch)
     assert not (st & capi.STATUS_NONFINITE).any()
     eq = np.abs(q - qr) / (np.abs(qr) + 1)
     ep = np.abs(p - pr) / (np.abs(pr) + 1)
@@ -59,7 +59,7 @@ def test_threshold_batches_match_register_window_and_oracle(gpu_lib, monkeypatch
 
 
 @pytest.mark.parametrize("side", [32, 64])
-@pytest.mark.parametrize("kernel", ["tiledl1", "tiledl4"])
+@pytest.mark.parametrize("kernel", ["lane1", "lane4"])
 def test_other_image_sides_vs_oracle(gpu_lib, monkeypatch, side, kernel):
     capi = gpu_lib
     wl = workloads.make("C2", n_chains=6)
@@ -86,7 +86,7 @@ def test_other_image_sides_vs_oracle(gpu_lib, monkeypatch, side, kernel):
     ctx.close()
 
 
-@pytest.mark.parametrize("kernel", ["tiledl1", "tiledl4"])
+@pytest.mark.parametrize("kernel", ["lane1", "lane4"])
 def test_nonfinite_chain_is_confined(gpu_lib, monkeypatch, kernel):
     """Bit-identical results for every other chain with and without the NaN
     chain.  (Not asserted for the register-window kernel: its factor

@@ -1,6 +1,6 @@
 """The fused one-star MH loop (mh_k1_tiledr, rhmc_mhk1.hpp: every iteration of
 run_RHMC's move-0 branch, sampler_RHMC.py:1018-1083, in one launch) against
-the four-kernel loop (RHMC_MH=unfused: mh_begin / leapfrog / energy / mh_end)
+the four-kernel loop (RHMC_OPT_MH_FUSED = 0: mh_begin / leapfrog / energy / mh_end)
 and the CPU oracle, at the bench's C2 geometry and on a 32-px image:
 
 * host randoms (the exact-parity mode): identical accept sequences, chains to
@@ -26,12 +26,16 @@ N_ITER, N_STEPS = 8, 25
 
 
 def _run(ctx, P, q0, z, u, monkeypatch, fused, seed=0):
-    if not fused:
-        monkeypatch.setenv("RHMC_MH", "unfused")
+    ctx.set_option(ctx_opt(), int(bool(fused)))
     try:
         return ctx.mh(P, q0, N_ITER, N_STEPS, f_pos=True, z=z, u=u, seed=seed)
     finally:
-        monkeypatch.delenv("RHMC_MH", raising=False)
+        ctx.set_option(ctx_opt(), 1)
+
+
+def ctx_opt():
+    from rhmc_amd import capi
+    return capi.OPT_MH_FUSED
 
 
 @pytest.fixture(scope="module")

@@ -21,14 +21,17 @@ def _ctx(capi, z):
     return capi.Context(z["D"])
 
 
-@pytest.fixture(params=["auto", "generic", "windowed", "tiledk", "tiledrk", "tiledrk_notab", "pixk", "tiled1", "tiled2", "tiledw", "tiledw32", "tiledr64", "tiledl1", "tiledl4", "tiledl1_64"])
+KERNEL_PATHS = ["auto", "generic", "windowed", "multiwin", "multiwin_notab", "pixmajor",
+                "regwin", "regwin32", "regwin_f64", "lane1", "lane4", "lane1_f64"]
+
+
+@pytest.fixture(params=KERNEL_PATHS)
 def kernel_path(request, monkeypatch):
-    """Run a test on the automatically chosen kernel, then again forced onto
-    the generic LDS-image kernel and onto the windowed large-image kernel."""
-    if request.param != "auto":
-        monkeypatch.setenv("RHMC_KERNEL", request.param)
-    else:
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
+    """Run a test on the automatically chosen kernel, then again with every
+    context it creates forced onto each kernel family (RHMC_OPT_KERNEL; a
+    family that does not serve a case leaves the automatic choice)."""
+    from rhmc_amd import capi
+    monkeypatch.setattr(capi, "DEFAULT_KERNEL", request.param)
     return request.param
 
 

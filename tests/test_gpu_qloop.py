@@ -38,15 +38,12 @@ def _oracle(wl, cm):
     return out
 
 
-@pytest.mark.parametrize("kernel", ["auto", "tiledr32", "tiledr64"])
+@pytest.mark.parametrize("kernel", ["auto", "regwin32", "regwin_f64"])
 @pytest.mark.parametrize("cm", [1, 2, 3, 7, 8, 9, 16, 1000])
 def test_fixed_point_pass_boundaries(gpu_lib, monkeypatch, kernel, cm):
     capi = gpu_lib
     from rhmc_amd import workloads
-    if kernel == "auto":
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
-    else:
-        monkeypatch.setenv("RHMC_KERNEL", kernel)
+    monkeypatch.setattr(capi, "DEFAULT_KERNEL", kernel)
     wl = workloads.make("C2", n_chains=CHAINS)
     par = dict(wl.params, dt=DT, delta=DELTA, counter_max=cm)
     ctx = capi.Context(wl.D)

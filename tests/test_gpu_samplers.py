@@ -120,7 +120,7 @@ def test_HMC_random_batched(gpu_lib):
 def test_hmc_random_register_window_vs_oracle_and_windowed(gpu_lib, side, wall, monkeypatch):
     """One star on a 32/48/64-px image takes the register-window kernel
     (hmc_random_k1_tiledr): trajectories against the oracle and the windowed
-    kernel (RHMC_KERNEL=windowed) to 1e-10, identical stale-momentum flags,
+    kernel (kernel option "windowed") to 1e-10, identical stale-momentum flags,
     ragged batch (the last wave partly empty, lengths differing inside a wave)."""
     from oracle import rhmc_ref as R
     capi = gpu_lib
@@ -148,9 +148,9 @@ def test_hmc_random_register_window_vs_oracle_and_windowed(gpu_lib, side, wall, 
     ctx = capi.Context(D)
     try:
         q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
-        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        ctx.set_kernel("windowed")
         qw, pw, stw = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
-        monkeypatch.delenv("RHMC_KERNEL")
+        ctx.set_kernel("auto")
         qs, ps = ctx.hmc_random(P, dt, q0[5:18], p0[5:18], steps[5:18])
     finally:
         ctx.close()
@@ -199,9 +199,9 @@ def test_hmc_random_many_stars_vs_oracle_and_windowed(gpu_lib, side, K, n, monke
     ctx = capi.Context(wl.D)
     try:
         q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
-        monkeypatch.setenv("RHMC_KERNEL", "windowed")
+        ctx.set_kernel("windowed")
         qw, pw, stw = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
-        monkeypatch.delenv("RHMC_KERNEL")
+        ctx.set_kernel("auto")
         idx = np.arange(min(n, 7))
         qs, ps = ctx.hmc_random(P, dt, q0[idx], p0[idx], steps[idx])
     finally:

@@ -6,7 +6,7 @@ paths (SURVEY §8(a) a6 and §8(f) next-3 through the C-ABI):
   pixel-major kernel is full-image, so the implicit step (rhmc_leapfrog), the
   explicit integrators (rhmc_integrate) and HMC_random (rhmc_hmc_random) all
   take it and agree with the oracle (no window_unsupported error);
-* RHMC_KERNEL=tiledrk forces the window-major kernel (leapfrog_kr with
+* the "multiwin" kernel option forces the window-major kernel (leapfrog_kr with
   kSolverHmcRandom) for HMC_random at K <= 10, where the default is the
   pixel-major kernel: both agree with the oracle and with each other.
 Tolerances as tests/test_gpu_parity.py: 1e-9 (q) / 1e-8 (p) relative to
@@ -57,7 +57,6 @@ def wide(gpu_lib):
 
 def test_wide_psf_implicit_vs_oracle(wide, monkeypatch):
     capi, D, q0, p0, par, ctx = wide
-    monkeypatch.delenv("RHMC_KERNEL", raising=False)
     P = capi.make_params(**par)
     n = 40
     q, p, it, st = ctx.leapfrog(P, q0, p0, n, return_info=True)
@@ -73,7 +72,6 @@ def test_wide_psf_implicit_vs_oracle(wide, monkeypatch):
 @pytest.mark.parametrize("name", ["hmc", "naive", "leap_frog"])
 def test_wide_psf_explicit_vs_oracle(wide, name, monkeypatch):
     capi, D, q0, p0, par, ctx = wide
-    monkeypatch.delenv("RHMC_KERNEL", raising=False)
     sid = {"hmc": capi.SOLVER_HMC, "naive": capi.SOLVER_RHMC_NAIVE,
            "leap_frog": capi.SOLVER_RHMC_LEAPFROG}[name]
     P = capi.make_params(**par)
@@ -108,7 +106,6 @@ def _hmc_random_case(par, q0, seed):
 
 def test_wide_psf_hmc_random_vs_oracle(wide, monkeypatch):
     capi, D, q0, _, par, ctx = wide
-    monkeypatch.delenv("RHMC_KERNEL", raising=False)
     hp, f_lim, p0, dt, steps = _hmc_random_case(par, q0, 5)
     P = capi.make_params(**hp)
     q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
@@ -123,20 +120,19 @@ def test_wide_psf_hmc_random_vs_oracle(wide, monkeypatch):
 @pytest.mark.parametrize("side,K,n", [(48, 10, 131), (32, 4, 67)])
 def test_hmc_random_window_major_forced(gpu_lib, side, K, n, monkeypatch):
     """K <= 10 on a 32/48-px image: pixel-major by default, window-major
-    (leapfrog_kr) under RHMC_KERNEL=tiledrk; both against the oracle."""
+    (leapfrog_kr) under the "multiwin" kernel option; both against the oracle."""
     capi = gpu_lib
     D, q0, _, par = _field(side, K, n, 7 + K, 3.4999999999999996)
     hp, f_lim, p0, dt, steps = _hmc_random_case(par, q0, K)
     P = capi.make_params(**hp)
     ctx = capi.Context(D)
     try:
-        monkeypatch.delenv("RHMC_KERNEL", raising=False)
         q, p, st = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
-        monkeypatch.setenv("RHMC_KERNEL", "tiledrk")
+        ctx.set_kernel("multiwin")
         qk, pk, stk = ctx.hmc_random(P, dt, q0, p0, steps, return_status=True)
         idx = np.arange(9)
         qs, ps = ctx.hmc_random(P, dt, q0[idx], p0[idx], steps[idx])
-        monkeypatch.delenv("RHMC_KERNEL")
+        ctx.set_kernel("auto")
     finally:
         ctx.close()
     np.testing.assert_array_equal(qs, qk[idx])         # window-major: batch invariance
