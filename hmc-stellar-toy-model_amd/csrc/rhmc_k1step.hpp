@@ -98,8 +98,12 @@ __device__ __forceinline__ double row_shr1(double v) {  // lane l of a 16-lane r
 // (np.max |q_j - q_{j+1}| > delta, NaN stops, counter_max) is evaluated in lane
 // j; a ballot gives the first stopping iteration k of each chain, whose state
 // q_{k+1} is read from lane k (ds_bpermute).  A chain with no stop among the 8
-// takes q_8 and runs another pass.  Same iterates, counts and cap status as
-// the sequential loop; one rcp chain per 8 iterations instead of per iteration.
+// takes q_8 and runs another pass.  The iterates agree with the sequential
+// loop's (and the reference's divide-form ones) to a few ulp, so the counts and
+// cap status are the reference's except where an iterate's max |dq| lies
+// within those few ulp of delta: there the loop can stop one iteration
+// earlier or later (tests/test_gpu_delta_edge.py bounds that case).  One rcp
+// chain per 8 iterations instead of per iteration.
 __device__ __forceinline__ void q_loop_lanes16(double& f, double& x, double& y, double bf,
                                                double cf, double bx, double cx, double by,
                                                double cy, const Consts& c, const LeanConsts& lc,

@@ -61,3 +61,39 @@ def test_psf_widths_either_side_of_the_range_guard(gpu_lib, monkeypatch, fwhm):
     q0[3, 1] = 2.2                          # one clamped window
     p0 = rng.randn(*q0.shape) * np.sqrt(workloads.metric_diag(q0, par))
     _check(gpu_lib, D, par, q0, p0, 30)
+
+
+@pytest.mark.parametrize("kernel", ["pixmajor", "multiwin"])
+def test_many_star_far_chain_and_narrow_psf(gpu_lib, kernel):
+    """The multi-star kernels' factor tables by recurrence (PixK::tables_rec)
+    fall back to direct exps when a run starts outside rec_vmax: a chain whose
+    star sits far outside the image (x = 300) and a narrow PSF (FWHM 1.2 px)
+    with 2 <= K <= 10, both chains of the wave against the oracle."""
+    capi = gpu_lib
+    from rhmc_amd.photometry import mag2flux
+    for fwhm in (3.4999999999999996, 1.2):
+        par, ftc = workloads.base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
+        par["fwhm_pix"] = fwhm
+        rng = np.random.RandomState(5)
+        K = 4
+        stars = [(17. + k, 10. + 8 * k, 30. - 5 * k) for k in range(K)]
+        D = workloads._image(48, stars, ftc, par["B_count"], fwhm, rng)
+        n = 4
+        q0 = np.empty((n, 3 * K))
+        q0[:, 0::3] = [mag2flux(s[0]) * ftc for s in stars]
+        q0[:, 1::3] = [s[1] for s in stars]
+        q0[:, 2::3] = [s[2] for s in stars]
+        q0 *= 1 + 0.01 * rng.randn(n, 3 * K)
+        q0[1, 1] = 300.0                    # chain 1 (wave-mate of chain 0): far out
+        q0[2, 5] = -280.0                   # chain 2: far out in y
+        p0 = rng.randn(n, 3 * K) * np.sqrt(workloads.metric_diag(q0, par))
+        ctx = capi.Context(D, kernel=kernel)
+        P = capi.make_params(**par)
+        q, p, it, st = ctx.leapfrog(P, q0, p0, 20, return_info=True)
+        ctx.close()
+        m = R.RefModel(D, dict(par, rows=48, cols=48))
+        for c in range(n):
+            qo, po, NP, NQ = m.trajectory(q0[c], p0[c], 20, record=False)
+            assert it[c, 0] == NP.sum() and it[c, 1] == NQ.sum(), (fwhm, c)
+            assert_state_close(q[c], qo, 1e-9, "q fwhm %g chain %d" % (fwhm, c))
+            assert_state_close(p[c], po, 1e-8, "p fwhm %g chain %d" % (fwhm, c))
