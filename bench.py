@@ -17,9 +17,9 @@ Extra objects on the JSON line:
                 bytes per launch (PMC), `hbm_measured_frac` its rate over
                 8 TB/s; `alg_model` = SURVEY §8(d)'s algorithmic-bytes model
                 (above the HBM peak by construction: D lives in LDS/VGPRs).
-  cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on every core of the
-                affinity mask, one chain per worker process, ~10 s per worker
-                (rank 0, N=1 only).
+  cpu_baseline  the NumPy CPU port (oracle/rhmc_ref.py) on all the host CPU the
+                job may use (affinity mask, capped by the cgroup CPU quota),
+                one chain per worker process, ~10 s per worker (rank 0, N=1).
   end_to_end    (leapfrog mode, N=1) the host-buffer C-ABI call rhmc_leapfrog
                 on the same chains: H2D + fused launch + D2H, synchronous — the
                 PCIe-inclusive rate a NumPy caller sees; never `value`.
@@ -88,25 +88,27 @@ def cpu_quota_cores():
 
 
 def cpu_baseline(wl, seconds_per_worker=10.0):
-    """Time the NumPy port on every host core this process may run on: one
-    chain per worker process (multiprocessing.Pool, OMP_NUM_THREADS=1), one
-    worker per core of the affinity mask, each running >= ~10 s."""
+    """Time the NumPy port on all the host CPU this process may use: one chain
+    per worker process (multiprocessing.Pool, OMP_NUM_THREADS=1), each worker
+    running ~10 s.  Workers = the CPUs of the affinity mask, or the cgroup's
+    CPU quota when that is smaller: the GPU box shows 256 CPUs in the mask but
+    grants 16 CPUs of time, and 256 time-sliced workers measured 4.1e4
+    chain-steps/s against 9.3e4 for 16 — the quota-sized pool
+    is the whole host available to the job."""
     import multiprocessing as mp
     os.environ["OMP_NUM_THREADS"] = "1"
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
         avail = os.cpu_count()
-    workers = max(1, avail)
     quota = cpu_quota_cores()
+    workers = max(1, min(avail, int(round(quota)) if quota else avail))
     par = dict(wl.params)
     par["rows"] = par["cols"] = wl.D.shape[0]
     # calibrate one chain on one idle core
     t = _cpu_worker((wl.D, par, wl.q0[0], wl.p0[0], 20))
     per_step = t / 20
-    # a cgroup quota below the worker count stretches every worker's wall time
-    share = min(1.0, quota / workers) if quota else 1.0
-    nsteps = max(20, int(seconds_per_worker * share / per_step))
+    nsteps = max(20, int(seconds_per_worker / per_step))
     jobs = [(wl.D, par, wl.q0[c % wl.n_chains], wl.p0[c % wl.n_chains], nsteps)
             for c in range(workers)]
     ctx = mp.get_context("fork")
@@ -125,9 +127,10 @@ def cpu_baseline(wl, seconds_per_worker=10.0):
             "kind": "port", "worker_seconds_min": min(worker_s),
             "one_core_value": 1.0 / per_step,
             "sample": "%d chains x %d steps of %s geometry, NumPy port of RHMC_single_step "
-                      "(oracle/rhmc_ref.py), one chain per worker process on each of the %d "
-                      "cores of the affinity mask, %s"
-                      % (len(jobs), nsteps, wl.name, workers, model)}
+                      "(oracle/rhmc_ref.py), one chain per worker process, %d workers = "
+                      "min(affinity CPUs %d, cgroup CPU quota %s), %s"
+                      % (len(jobs), nsteps, wl.name, workers, avail,
+                         "none" if quota is None else "%g" % quota, model)}
 
 
 def _free_port():

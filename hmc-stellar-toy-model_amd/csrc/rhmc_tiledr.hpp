@@ -65,6 +65,12 @@ constexpr int kRcpGroup = RHMC_RCP_GROUP;
 #define RHMC_FACT_REC 1
 #endif
 
+// Fold each row sum R_i into the moments as soon as its row is complete
+// (same summation order; frees the row-sum registers during the pixel loop).
+#ifndef RHMC_RFOLD
+#define RHMC_RFOLD 1
+#endif
+
 // DT: the type the window pixels are cached in (float when the image is
 // exactly representable in fp32, else double).
 //
@@ -224,6 +230,26 @@ struct TiledR {
     const double w0 = (k.c0 + ((double)a + 0.5)) - y;                // column a
     const bool ok = fabs(v0) < lc.rec_vmax && fabs(w0) < lc.rec_vmax;
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
+      factors_from(etab, v0, w0, lc, scale, ex, ey);
+      return;
+    }
+#endif
+    factors(etab, k, x, y, lc, ex, ey);
+#pragma unroll
+    for (int j = 0; j < TC; ++j) ey[j] = scale * ey[j];
+  }
+
+  // The recurrence of factors_rec from the lane's row-group / column offsets
+  // v0, w0 (in range for every chain of the wave).
+  static __device__ __forceinline__ void factors_from(const double* __restrict__ etab, double v0,
+                                                      double w0, const LeanConsts& lc,
+                                                      double scale, double (&ex)[TR],
+                                                      double (&ey)[TC]) {
+    {
+      const int lane = lane_id();
+      const int m = lane % LPC;
+      const int b = m % 4;
+      const double c = lc.inv_two_sig2;
       const double z = (b < 2) ? v0 : w0;
       const double lin = (b < 2) ? fma(2.0, z, 1.0) : fma(8.0, z, 16.0);
       const double t = ((b & 1) ? lin : z * z) * -c;
@@ -246,12 +272,7 @@ struct TiledR {
         ey[j] = ey[j - 1] * h;
         if (j + 1 < TC) h = h * lc.k_col4;
       }
-      return;
     }
-#endif
-    factors(etab, k, x, y, lc, ex, ey);
-#pragma unroll
-    for (int j = 0; j < TC; ++j) ey[j] = scale * ey[j];
   }
 
   // The window's part of the chain's potential V (sampler_RHMC.py:294-302,
@@ -307,11 +328,11 @@ struct TiledR {
     gmark(-1);
     const int m = lane_id() % LPC;
     const int a = m / 4, b = m % 4;
+    double ex[TR], ey[TC];
     ensure(sD, k, x, y);
     gmark(3);
-    const double r0 = k.r0, c0 = k.c0;
-    double ex[TR], ey[TC];
     factors_rec(etab, k, x, y, lc, f, ex, ey);  // ey carries f
+    const double r0 = k.r0, c0 = k.c0;
     gmark(0);
 
     // s_ij = D_ij / Lambda_ij - 1 with one reciprocal per group of kRcpGroup
@@ -319,6 +340,13 @@ struct TiledR {
     // 1/l0 = l1 l2 l3 r etc. by products (v_rcp_f64 issues at a quarter of the
     // FMA rate); then the separable row / column sums (rhmc_tiled2.hpp).
     double R[TR], C[TC];
+    // a0 = sum_i ex_i R_i is also sum_j fey_j C_j: it serves both moments
+    double a0 = 0.0, a1 = 0.0, w1 = 0.0;
+    auto fold = [&](int i) {  // row i's sum into the moments (in row order)
+      const double tt = ex[i] * R[i];
+      a0 += tt;
+      if (i > 0) a1 = fma(tt, (double)i, a1);
+    };
     auto lam = [&](int pp) {  // Lambda at pixel pp (:373-376)
       return fma(ex[pp / TC], ey[pp % TC], c.B);
     };
@@ -326,6 +354,7 @@ struct TiledR {
       const int i = pp / TC, j = pp % TC;
       R[i] = (j == 0) ? ey[j] * sv : fma(ey[j], sv, R[i]);
       C[j] = (i == 0) ? ex[i] * sv : fma(ex[i], sv, C[j]);
+      if (RHMC_RFOLD && j == TC - 1) fold(i);
     };
     auto rcpn = [](double L) {
       const double r = __builtin_amdgcn_rcp(L);
@@ -363,13 +392,9 @@ struct TiledR {
       acc(pp, fma((double)k.d[pp], rcpn(lam(pp)), -1.0));
     }
     gmark(1);
-    // a0 = sum_i ex_i R_i is also sum_j fey_j C_j: it serves both moments
-    double a0 = 0.0, a1 = 0.0, w1 = 0.0;
+    if (!RHMC_RFOLD) {
 #pragma unroll
-    for (int i = 0; i < TR; ++i) {
-      const double tt = ex[i] * R[i];
-      a0 += tt;
-      if (i > 0) a1 = fma(tt, (double)i, a1);
+      for (int i = 0; i < TR; ++i) fold(i);
     }
 #pragma unroll
     for (int j = 1; j < TC; ++j) w1 = fma(ey[j] * C[j], (double)(4 * j), w1);

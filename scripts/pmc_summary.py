@@ -18,17 +18,21 @@ root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_c2"
 wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
 kernel_sub = sys.argv[3] if len(sys.argv) > 3 else "leapfrog"
 chain_steps = float(sys.argv[4]) if len(sys.argv) > 4 else 4096 * 500.
+head = sys.argv[5] if len(sys.argv) > 5 else None      # source revision measured
 
 vals = defaultdict(list)
+names = set()
 for path in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), recursive=True):
     with open(path) as fh:
         for row in csv.DictReader(fh):
             if kernel_sub not in row.get("Kernel_Name", ""):
                 continue
+            names.add(row["Kernel_Name"])
             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
 
 avg = {k: sum(v) / len(v) for k, v in vals.items() if v}
-out = {"workload": wl, "kernel_filter": kernel_sub, "counters_avg_per_dispatch": avg}
+out = {"workload": wl, "kernel_filter": kernel_sub, "kernel": " | ".join(sorted(names)),
+       "head": head, "counters_avg_per_dispatch": avg}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     out["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
 f64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")
