@@ -33,6 +33,7 @@
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
 #include "rhmc_mhk1.hpp"
+#include "rhmc_mhpk.hpp"
 #include "rhmc_pixk.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
@@ -1309,6 +1310,36 @@ int launch_mh_k1(const rhmc_ctx* ctx, MhK1Args k, hipStream_t s) {
   return RHMC_OK;
 }
 
+// 2 <= K <= 10 stars where launch_leapfrog takes the pixel-major kernel: one
+// launch per MH iteration instead of four (rhmc_mhpk.hpp).  RHMC_OPT_MH_FUSED
+// = 0, or a forced kernel other than PIXMAJOR, keeps the four-kernel loop.
+bool mh_pk_fused(const rhmc_ctx* ctx, const Consts& c, int K) {
+  if (!ctx->mh_fused) return false;
+  if (ctx->kernel != RHMC_KERNEL_AUTO && ctx->kernel != RHMC_KERNEL_PIXMAJOR) return false;
+  return use_pixk(ctx, K, c);
+}
+
+// V(q) once, then one mh_pk_iter launch per iteration (rhmc_mhpk.hpp); V
+// [n] is the carried V(q) (device scratch).
+template <int IMG>
+int launch_mh_pk(const rhmc_ctx* ctx, MhKArgs k, double* V, hipStream_t s) {
+  using MP = MhPK<IMG, 10>;
+  int W = 4;
+  while (W > 1 && MP::lds_bytes(W) > (size_t)ctx->max_lds / 2) W >>= 1;
+  const size_t lds = MP::lds_bytes(W);
+  if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "mh_pk LDS");
+  k.Df = ctx->d_Df;
+  const int64_t waves = (k.n + MP::PK::CPW - 1) / MP::PK::CPW;
+  const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
+  hipLaunchKernelGGL((mh_pk_v0<IMG, 10>), grid, block, lds, s, k, V);
+  HIP_TRY(hipGetLastError());
+  for (int it = 0; it < k.n_iter; ++it) {
+    hipLaunchKernelGGL((mh_pk_iter<IMG, 10>), grid, block, lds, s, k, it, V);
+    HIP_TRY(hipGetLastError());
+  }
+  return RHMC_OK;
+}
+
 // The MH outer loop on device buffers (sampler_RHMC.py:1018-1083): per
 // iteration begin -> n_steps fused leapfrog -> V(q') -> accept, all queued on
 // `s` with no host synchronisation.  `rec` holds device pointers (nullable).
@@ -1344,6 +1375,36 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
       case 48: return launch_mh_k1<48>(ctx, k, s);
       default: return launch_mh_k1<64>(ctx, k, s);
     }
+  }
+  if (K >= 2 && mh_pk_fused(ctx, c, K)) {
+    MhKArgs k;
+    k.q = d_q;
+    k.Df = nullptr;
+    k.z = d_z;
+    k.u = d_u;
+    k.q_chain = rec ? rec->q_chain : nullptr;
+    k.E_chain = rec ? rec->E_chain : nullptr;
+    k.V_chain = rec ? rec->V_chain : nullptr;
+    k.T_chain = rec ? rec->T_chain : nullptr;
+    k.accept = rec ? rec->accept : nullptr;
+    k.n = n;
+    k.K = K;
+    k.n_iter = n_iter;
+    k.n_steps = n_steps;
+    k.f_pos = f_pos != 0 ? RHMC_V_FLUX_WALL : 0;
+    k.seed = seed;
+    k.c = c;
+    const size_t need = (size_t)n * sizeof(double) + 256;
+    if (need > ctx->mh_scratch_bytes) {
+      if (ctx->mh_scratch) HIP_TRY(hipFree(ctx->mh_scratch));
+      ctx->mh_scratch = nullptr;
+      ctx->mh_scratch_bytes = 0;
+      if (hipMalloc(&ctx->mh_scratch, need) != hipSuccess)
+        return fail(RHMC_ERR_NOMEM, "hipMalloc MH scratch failed");
+      ctx->mh_scratch_bytes = need;
+    }
+    double* V = (double*)ctx->mh_scratch;
+    return ctx->rows == 32 ? launch_mh_pk<32>(ctx, k, V, s) : launch_mh_pk<48>(ctx, k, V, s);
   }
   const size_t sb = (size_t)n * 3 * K * sizeof(double), eb = (size_t)n * sizeof(double);
   const size_t need = 2 * sb + 3 * eb + 256;

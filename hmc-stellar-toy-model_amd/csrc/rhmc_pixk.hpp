@@ -263,16 +263,13 @@ struct PixK {
     return true;
   }
 
-  // Pixel part of dphidq (:365-425 without metric / prior): lane m < K gets
-  // star m's; the star table `tab` holds the chain's (f, x, y).
-  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
-                                                  const float* __restrict__ simg,
-                                                  const KRStar* tab, double* rtab, int K,
-                                                  const Consts& c, const LeanConsts& lc,
-                                                  double& gf, double& gx, double& gy) {
+  // The chain's factor tables ex [IMG][KMAX] (rtab) and fey (ctab) for the
+  // stars in `tab`: by recurrence, or every entry directly when a run of the
+  // wave is out of the recurrence's range.
+  static __device__ __forceinline__ void tables(const double* __restrict__ etab,
+                                                const KRStar* tab, double* rtab, double* ctab,
+                                                int K, const LeanConsts& lc) {
     const int m = lane_id() & (LPC - 1);
-    double* ctab = rtab + (size_t)IMG * KMAX;
-    wave_lds_sync();  // the previous gradient's table reads are done
 #if RHMC_PK_REC
     if (!tables_rec(etab, tab, rtab, ctab, K, lc))
 #endif
@@ -288,6 +285,19 @@ struct PixK {
       rtab[e] = ex;
       ctab[e] = fey;
     }
+  }
+
+  // Pixel part of dphidq (:365-425 without metric / prior): lane m < K gets
+  // star m's; the star table `tab` holds the chain's (f, x, y).
+  static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
+                                                  const float* __restrict__ simg,
+                                                  const KRStar* tab, double* rtab, int K,
+                                                  const Consts& c, const LeanConsts& lc,
+                                                  double& gf, double& gx, double& gy) {
+    const int m = lane_id() & (LPC - 1);
+    double* ctab = rtab + (size_t)IMG * KMAX;
+    wave_lds_sync();  // the previous gradient's table reads are done
+    tables(etab, tab, rtab, ctab, K, lc);
     wave_lds_sync();
     double A0[KMAX], A1[KMAX], A2[KMAX];
 #pragma unroll
