@@ -278,6 +278,8 @@ def main():
                          "datagen: --n-real Poisson realisations of the workload's model "
                          "image (rhmc_gen_image)")
     ap.add_argument("--mh-iter", type=int, default=10)
+    ap.add_argument("--mh-unfused", action="store_true",
+                    help="--mode mh: the four-kernel loop (RHMC_OPT_MH_FUSED = 0)")
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
     ap.add_argument("--n-real", type=int, default=1000)
     ap.add_argument("--dry-run", action="store_true",
@@ -351,6 +353,8 @@ def main():
         return bench_datagen(args, wl, P, ctx, dev, stream, world, rank)
     if args.mode == "mh":
         leap = args.leap or 10
+        if args.mh_unfused:
+            ctx.set_option(capi.OPT_MH_FUSED, 0)
 
         def launch():
             ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap, f_pos=True,
@@ -442,6 +446,7 @@ def main():
                    "chains_per_gpu": wl.n_chains, "total_chains": total_chains,
                    "image": list(wl.D.shape), "K": wl.K,
                    "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
+                   "mh_fused": (None if args.mode != "mh" else not args.mh_unfused),
                    "solver": (args.solver if args.mode == "integrate" else
                               "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},

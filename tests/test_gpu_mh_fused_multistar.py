@@ -41,6 +41,9 @@ def _close(a, b, rel, what):
 @pytest.fixture(scope="module")
 def c3(gpu_lib):
     wl = workloads.make("C3", n_chains=1001)
+    # C3's power-law fluxes reach below the wall (f_lim): V(q0) = inf there and
+    # every proposal would be rejected; start the MH chains above it
+    wl.q0[:, 0::3] = np.maximum(wl.q0[:, 0::3], 1.5 * wl.params["f_lim"])
     ctx = gpu_lib.Context(wl.D)
     rng = np.random.RandomState(19)
     z = rng.randn(N_ITER, wl.n_chains, 3 * wl.K)
