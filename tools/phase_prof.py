@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Per-phase cycle split of the single-star kernels (tools only).
+"""Per-phase cycle split of the register-window kernel (tools only).
 
-RHMC_KERNEL=profr  register-window kernel: cycles per step per wave in the
-                   gradient, kicks + reflection + p-loop, q-loop, and flux
-                   metric + closing update (fenced s_memtime reads; the PROF
-                   build writes them over the chain state).
-RHMC_KERNEL=profw16|profw32  LDS-window kernel: gradient vs the rest.
-usage: RHMC_KERNEL=profr python tools/phase_prof.py [n_chains]
+Needs the phase-timing library: `make -C hmc-stellar-toy-model_amd prof`
+(-DRHMC_PHASE_PROF -> build/variants/lib_prof.so), whose register-window
+launches write cycles per step per wave over the chain state: the gradient,
+kicks + reflection + p-loop, q-loop, flux metric + closing update, and inside
+the gradient the window check, PSF factors, pixel loop and moments +
+reductions (fenced s_memtime reads).
+usage: RHMC_LIB=build/variants/lib_prof.so python tools/phase_prof.py [n_chains]
 """
 import os
 import sys
@@ -18,7 +19,7 @@ import torch  # noqa: E402
 from rhmc_amd import capi, workloads  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-kern = os.environ.get("RHMC_KERNEL", "")
+kern = "profr"
 wl = workloads.make("C2", n_chains=n)
 P = capi.make_params(**wl.params)
 ctx = capi.Context(wl.D)
