@@ -153,7 +153,7 @@ __device__ __forceinline__ void mh_pk_load(const double* q, const MhPkIds& id, i
   s.f = own ? q[e] : 1.0;
   s.x = own ? q[e + 1] : 0.0;
   s.y = own ? q[e + 2] : 0.0;
-  s.pad = 0.0;
+  s.pad = flux_fold(s.f);
   tab[id.m] = s;
 }
 

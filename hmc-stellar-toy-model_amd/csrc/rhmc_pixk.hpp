@@ -239,7 +239,7 @@ struct PixK {
     }
     if (__builtin_amdgcn_ballot_w64(!ok) != 0) return false;
     if (!act) return true;
-    const double fn = real ? st.f * lc.inv_norm : 0.0;
+    const double fn = real ? st.pad * lc.inv_norm : 0.0;  // pad = flux_fold(f) (kr_publish)
 #pragma unroll 1
     for (int t = 0; t < 2; ++t) {  // t = 0: row table ex, t = 1: column table fey
       const double ctr = t ? ys : xs;
@@ -280,7 +280,7 @@ struct PixK {
         const double v = ((double)i + 0.5) - tab[k].x;
         ex = exp_neg(-(v * v) * lc.inv_two_sig2, etab);
         const double u = ((double)i + 0.5) - tab[k].y;
-        fey = tab[k].f * (exp_neg(-(u * u) * lc.inv_two_sig2, etab) * lc.inv_norm);
+        fey = tab[k].pad * (exp_neg(-(u * u) * lc.inv_two_sig2, etab) * lc.inv_norm);
       }
       rtab[e] = ex;
       ctab[e] = fey;
@@ -322,7 +322,7 @@ struct PixK {
     gf = gx = gy = 0.0;
     if (m < K) {
       const KRStar st = tab[m];
-      gf = -s0 / st.f;                                      // :404
+      gf = -s0 / st.pad;                                    // :404 (pad = flux_fold(f))
       gx = -fma(kCtr - st.x, s0, s1) * lc.inv_var;          // :405
       gy = -fma(kCtr - st.y, s0, s2) * lc.inv_var;          // :406
     }
@@ -336,7 +336,7 @@ struct PixK {
         const double s2 = half_sum_dpp(A2[k]);
         if (m == k) {
           const KRStar st = tab[k];
-          gf = -s0 / st.f;                                  // :404
+          gf = -s0 / st.pad;                                // :404 (pad = flux_fold(f))
           gx = -fma(kCtr - st.x, s0, s1) * lc.inv_var;      // :405
           gy = -fma(kCtr - st.y, s0, s2) * lc.inv_var;      // :406
         }

@@ -57,7 +57,8 @@ struct LeapArgsKR {
 constexpr int kSolverHmcRandom = 100;
 
 struct KRStar {  // LDS star table entry
-  double f, x, y, pad;
+  double f, x, y;
+  double pad;     // flux_fold(f): the flux the pixel-major kernel folds into its factors
 };
 
 // TAB variant: Lambda over all stars in an unrolled loop (A/B knob), for at
@@ -392,7 +393,7 @@ __device__ __forceinline__ void kr_publish(KRStar* tab, const double (&f)[SLOTS]
       e.f = f[t];
       e.x = x[t];
       e.y = y[t];
-      e.pad = 0.0;
+      e.pad = flux_fold(f[t]);
       tab[32 * t + m] = e;
     }
   wave_lds_sync();

@@ -34,6 +34,17 @@ struct Consts {
   int counter_max, use_prior, use_Vc, pad;
 };
 
+// The flux folded into a star's PSF factors (the kernels scale the column
+// factors by f, so that one product serves Lambda and the sums, and divide the
+// flux sum by f again).  For |f| < 2^-500 (0 included) that fold would
+// underflow or give 0/0: such a star folds 2^-600 instead, an exact power of
+// two, so -sum psf (D/Lambda - 1) comes back exactly (:404) and Lambda still
+// rounds to what f psf gives (both below half an ulp of B).  The x, y sums
+// then carry 2^-600 for f: they differ from the reference's (f/var) sum by
+// less than 2^-600 relative to the sum — far below any momentum's ulp.
+__device__ __forceinline__ bool flux_tiny(double f) { return fabs(f) < 0x1p-500; }
+__device__ __forceinline__ double flux_fold(double f) { return flux_tiny(f) ? 0x1p-600 : f; }
+
 // A position reflection (v < 0 or v > edge, sampler_RHMC.py:561-564) whose
 // coordinate lies within 2^-40 (9.1e-13) of its wall, relative to max(1, wall)
 // (edge >= 1): RHMC_STATUS_NEAR_WALL.  Only meaningful when v
