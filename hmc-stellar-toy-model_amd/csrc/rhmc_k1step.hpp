@@ -27,6 +27,11 @@ namespace rhmc {
 #ifndef RHMC_SPEC_Q
 #define RHMC_SPEC_Q 2
 #endif
+// RHMC_STATUS_NEAR_WALL in the one-star step loop: 2 = flux wall and image
+// edges, 1 = flux wall only, 0 = off.
+#ifndef RHMC_NEAR_WALL
+#define RHMC_NEAR_WALL 2
+#endif
 constexpr int kSpecP = RHMC_SPEC_P;
 constexpr int kSpecQ = RHMC_SPEC_Q;
 
@@ -196,17 +201,17 @@ __device__ __forceinline__ void k1_steps(double& f, double& x, double& y, double
       if (f < c.f_lim) {                           // :554-564
         pf = -pf;
         st |= RHMC_STATUS_REFLECT_F;
-        if (f >= c.near_f) st |= RHMC_STATUS_NEAR_WALL;
+        if (RHMC_NEAR_WALL >= 1 && f >= c.near_f) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (x < 0.0 || x > edge) {
         px = -px;
         st |= RHMC_STATUS_REFLECT_XY;
-        if (near_edge(x, edge)) st |= RHMC_STATUS_NEAR_WALL;
+        if (RHMC_NEAR_WALL >= 2 && near_edge(x, edge)) st |= RHMC_STATUS_NEAR_WALL;
       }
       if (y < 0.0 || y > edge) {
         py = -py;
         st |= RHMC_STATUS_REFLECT_XY;
-        if (near_edge(y, edge)) st |= RHMC_STATUS_NEAR_WALL;
+        if (RHMC_NEAR_WALL >= 2 && near_edge(y, edge)) st |= RHMC_STATUS_NEAR_WALL;
       }
     }
     if (s == n_steps) {

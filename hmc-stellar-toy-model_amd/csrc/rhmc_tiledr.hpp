@@ -217,31 +217,25 @@ struct TiledR {
   // exp(-(dx^2 + dy^2) c) by a few ulp).  A wave with a chain so far from its
   // window that a base exp or a ratio could leave the fp64 range
   // (|v0| or |w0| >= rec_vmax, or NaN) takes the direct factors instead.
-  // Returns the scale folded into ey: `scale`, or flux_fold(scale) on the
-  // direct path.
-  static __device__ __forceinline__ double factors_rec(const double* __restrict__ etab,
-                                                       const Cache& k, double x, double y,
-                                                       const LeanConsts& lc, double scale,
-                                                       double (&ex)[TR], double (&ey)[TC]) {
+  static __device__ __forceinline__ void factors_rec(const double* __restrict__ etab,
+                                                     const Cache& k, double x, double y,
+                                                     const LeanConsts& lc, double scale,
+                                                     double (&ex)[TR], double (&ey)[TC]) {
 #if RHMC_FACT_REC
     const int lane = lane_id();
     const int m = lane % LPC;
-    const int a = m / 4, b = m % 4;
-    const double c = lc.inv_two_sig2;
+    const int a = m / 4;
     const double v0 = (k.r0 + ((double)(ROW0 + TR * a) + 0.5)) - x;  // row group a, first row
     const double w0 = (k.c0 + ((double)a + 0.5)) - y;                // column a
-    // a tiny flux (flux_fold) also takes the direct path, which folds 2^-600
-    const bool ok = fabs(v0) < lc.rec_vmax && fabs(w0) < lc.rec_vmax && !flux_tiny(scale);
+    const bool ok = fabs(v0) < lc.rec_vmax && fabs(w0) < lc.rec_vmax;
     if (__builtin_amdgcn_ballot_w64(!ok) == 0) {
       factors_from(etab, v0, w0, lc, scale, ex, ey);
-      return scale;
+      return;
     }
 #endif
     factors(etab, k, x, y, lc, ex, ey);
-    const double fs = flux_fold(scale);
 #pragma unroll
-    for (int j = 0; j < TC; ++j) ey[j] = fs * ey[j];
-    return fs;
+    for (int j = 0; j < TC; ++j) ey[j] = scale * ey[j];
   }
 
   // The recurrence of factors_rec from the lane's row-group / column offsets
@@ -308,7 +302,7 @@ struct TiledR {
   }
 
   // The row slice's sums of the chain's dphidq pixel terms, all three scaled
-  // by the flux fs = flux_fold(f) (returned): s0 = fs sum psf s, s1 = fs sum psf s dx,
+  // by the flux fs = flux_fold(f) (out): s0 = fs sum psf s, s1 = fs sum psf s dx,
   // s2 = fs sum psf s dy
   // (s = D/Lambda - 1; every lane of the chain gets them).  The column
   // factors carry f (fey = f ey serves Lambda and both sums), so no separate
@@ -337,7 +331,8 @@ struct TiledR {
     double ex[TR], ey[TC];
     ensure(sD, k, x, y);
     gmark(3);
-    fs = factors_rec(etab, k, x, y, lc, f, ex, ey);  // ey carries f (flux_fold(f))
+    fs = flux_fold(f);
+    factors_rec(etab, k, x, y, lc, fs, ex, ey);  // ey carries fs (= f but at |f| < 2^-547)
     const double r0 = k.r0, c0 = k.c0;
     gmark(0);
 
@@ -425,7 +420,7 @@ struct TiledR {
                                                   double& gy, long long* gp = nullptr) {
     double s0, s1, s2, fs;
     partial<PROFG>(etab, sD, k, f, x, y, c, lc, s0, s1, s2, fs, gp);
-    gf = -s0 * rcp_nr1(fs);                            // :404 (fs = flux_fold(f), f but for |f| < 2^-500)
+    gf = -s0 * rcp_nr1(fs);                            // :404 (fs = flux_fold(f): f but for |f| < 2^-547)
     gx = -s1 * lc.inv_var;                             // :405
     gy = -s2 * lc.inv_var;                             // :406
   }

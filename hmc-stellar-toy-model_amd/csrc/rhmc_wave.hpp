@@ -36,14 +36,18 @@ struct Consts {
 
 // The flux folded into a star's PSF factors (the kernels scale the column
 // factors by f, so that one product serves Lambda and the sums, and divide the
-// flux sum by f again).  For |f| < 2^-500 (0 included) that fold would
-// underflow or give 0/0: such a star folds 2^-600 instead, an exact power of
-// two, so -sum psf (D/Lambda - 1) comes back exactly (:404) and Lambda still
-// rounds to what f psf gives (both below half an ulp of B).  The x, y sums
-// then carry 2^-600 for f: they differ from the reference's (f/var) sum by
-// less than 2^-600 relative to the sum — far below any momentum's ulp.
-__device__ __forceinline__ bool flux_tiny(double f) { return fabs(f) < 0x1p-500; }
-__device__ __forceinline__ double flux_fold(double f) { return flux_tiny(f) ? 0x1p-600 : f; }
+// flux sum by f again).  At f = 0 that gives 0/0 where the reference's
+// -sum psf (D/Lambda - 1) (:404) is finite, and a subnormal f underflows.  The
+// fold is f pushed 2^-600 away from zero: copysign(|f| + 2^-600, f).  For
+// |f| >= 2^-547 that IS f (2^-600 is below half its ulp), so every ordinary
+// chain is bit-identical; for smaller |f| (0 included) the flux sum comes
+// back exactly by the division and Lambda still rounds to B as with f psf.
+// The x, y sums then carry the fold for f: they differ from the reference's
+// (f/var) sum by less than 2^-599 relative to the sum, far below any
+// momentum's ulp.  Two VALU instructions, no compare or branch.
+__device__ __forceinline__ double flux_fold(double f) {
+  return copysign(fabs(f) + 0x1p-600, f);
+}
 
 // A position reflection (v < 0 or v > edge, sampler_RHMC.py:561-564) whose
 // coordinate lies within 2^-40 (9.1e-13) of its wall, relative to max(1, wall)
