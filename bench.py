@@ -304,9 +304,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
     from rhmc_amd import shard, workloads
-    if args.workload.upper() == "C4" and not args.chains and not args.global_chains:
-        # C4 is one 2^20-chain set sharded over the ranks (BASELINE configs[3])
-        args.global_chains = 1 << 20
+    if args.workload.upper() in ("C4", "C5") and not args.chains and not args.global_chains:
+        # C4 is one 2^20-chain set, C5 one 8192-chain set, sharded over the
+        # ranks (BASELINE configs[3], [4]: "... across 8x MI355X")
+        args.global_chains = (1 << 20) if args.workload.upper() == "C4" else 8192
     if args.global_chains:
         # one global chain set (seed 1000), this rank's contiguous shard
         wl = workloads.make(args.workload, n_chains=args.global_chains)
@@ -526,6 +527,7 @@ def dry_run(args, wl, world, rank, gpu, total_chains):
         dist.destroy_process_group()
     if rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": world, "workload": wl.name,
+                          "scaling": "strong" if args.global_chains else "weak",
                           "config": {"chains_per_gpu": int(wl.n_chains),
                                      "total_chains": int(total_chains),
                                      "parallelism": "chain-sharded x%d" % world},

@@ -753,6 +753,7 @@ struct rhmc_ctx {
   int n_cu = 0;
   int kernel = RHMC_KERNEL_AUTO;   // RHMC_OPT_KERNEL
   int mh_fused = 1;                // RHMC_OPT_MH_FUSED
+  int window_split = 0;            // RHMC_OPT_WINDOW_SPLIT (0: by batch size)
 };
 
 namespace {
@@ -1109,18 +1110,40 @@ bool use_tiledrk(const rhmc_ctx* ctx, int K, const Consts& c) {
   return !per_wave_forced(ctx) && tiledrk_ok(ctx, K, c);
 }
 
-template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
-int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_t s) {
+template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT, int WS = 1>
+int launch_kr_ws(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_t s) {
   using TK = TiledRK<DT, SLOTS, TAB>;
   int W = 4;
-  while (W > 1 && TK::lds_bytes(W, a.K, a.side) > (size_t)ctx->max_lds / 2) W >>= 1;
-  const size_t lds = TK::lds_bytes(W, a.K, a.side);
+  while (W > WS && TK::lds_bytes(W, a.K, a.side, WS) > (size_t)ctx->max_lds / 2) W >>= 1;
+  const size_t lds = TK::lds_bytes(W, a.K, a.side, WS);
   if (lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "factor tables exceed LDS");
-  const int64_t waves = (a.n_chains + TK::CPW - 1) / TK::CPW;
+  const int64_t waves = (a.n_chains + TK::CPW - 1) / TK::CPW * WS;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS, TAB, SOLVER>), grid, block, lds, s, a, f_pos);
+  hipLaunchKernelGGL((leapfrog_kr<DT, SLOTS, TAB, SOLVER, WS>), grid, block, lds, s, a, f_pos);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
+}
+
+// Waves per chain pair for the implicit window-major kernel: the option, or
+// the least of 1, 2, 4 that puts two waves on every SIMD (4 per CU).
+int kr_window_split(const rhmc_ctx* ctx, int64_t n_chains) {
+  if (ctx->window_split) return ctx->window_split;
+  const int64_t pairs = (n_chains + 1) / 2, target = 8 * (int64_t)(ctx->n_cu > 0 ? ctx->n_cu : 256);
+  int ws = 1;
+  while (ws < 4 && pairs * ws < target) ws *= 2;
+  return ws;
+}
+
+template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
+int launch_kr_t(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_t s) {
+  if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT && !TAB) {
+    switch (kr_window_split(ctx, a.n_chains)) {
+      case 2: return launch_kr_ws<DT, SLOTS, TAB, SOLVER, 2>(ctx, a, f_pos, s);
+      case 4: return launch_kr_ws<DT, SLOTS, TAB, SOLVER, 4>(ctx, a, f_pos, s);
+      default: break;
+    }
+  }
+  return launch_kr_ws<DT, SLOTS, TAB, SOLVER, 1>(ctx, a, f_pos, s);
 }
 
 // Factor tables in LDS (TiledRK<..., TAB>) for images up to 64 px with K <= 16,
@@ -1830,6 +1853,11 @@ int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value) {
       if (value != 0 && value != 1) return fail(RHMC_ERR_ARG, "RHMC_OPT_MH_FUSED must be 0 or 1");
       ctx->mh_fused = value;
       return RHMC_OK;
+    case RHMC_OPT_WINDOW_SPLIT:
+      if (value != 0 && value != 1 && value != 2 && value != 4)
+        return fail(RHMC_ERR_ARG, "RHMC_OPT_WINDOW_SPLIT must be 0, 1, 2 or 4");
+      ctx->window_split = value;
+      return RHMC_OK;
     default:
       return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
   }
@@ -1840,6 +1868,7 @@ int rhmc_ctx_get_option(rhmc_ctx* ctx, int32_t option, int32_t* value) {
   switch (option) {
     case RHMC_OPT_KERNEL: *value = ctx->kernel; return RHMC_OK;
     case RHMC_OPT_MH_FUSED: *value = ctx->mh_fused; return RHMC_OK;
+    case RHMC_OPT_WINDOW_SPLIT: *value = ctx->window_split; return RHMC_OK;
     default: return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
   }
 }

@@ -112,11 +112,18 @@ struct TiledRK {
 
   // LDS: exp table, per-chain star tables, then (TAB) per-chain factor tables
   // and the image (DT [side][side], read by every window of the workgroup).
-  static __host__ __device__ constexpr size_t lds_bytes(int waves, int K, int side) {
+  // ws > 1 (window split, leapfrog_kr): per group of ws waves, two gradient
+  // exchange buffers [CPW][KMAX][3] after everything else.
+  static __host__ __device__ constexpr size_t xchg_doubles(int waves, int ws) {
+    return ws > 1 ? (size_t)(waves / ws) * 2 * CPW * KMAX * 3 : 0;
+  }
+  static __host__ __device__ constexpr size_t lds_bytes(int waves, int K, int side,
+                                                        int ws = 1) {
     return kExpTab * sizeof(double) + (size_t)waves * CPW * KMAX * sizeof(KRStar) +
            (TAB ? (size_t)waves * CPW * K * 2 * side * sizeof(double) +
                       (kImgLds ? (size_t)side * side * sizeof(DT) : 0)
-                : (size_t)waves * CPW * RED_DOUBLES * sizeof(double));
+                : (size_t)waves * CPW * RED_DOUBLES * sizeof(double)) +
+           xchg_doubles(waves, ws) * sizeof(double);
   }
   static __device__ __forceinline__ int origin(double v, int half, int omax) {
     if (!(fabs(v) < 1.0e7)) return 0;
@@ -187,6 +194,13 @@ struct TiledRK {
 
   // Pixel part of dphidq for every star of the chain (:365-425 without the
   // metric / prior terms): lane m receives stars m + 32 t in slot t.
+  // Window split (WS > 1): the WS waves of a group hold the same two chains
+  // (identical replicated state); wave wsub evaluates the windows of stars
+  // m = wsub (mod WS) and the group swaps the results through xb (this
+  // gradient's exchange buffer, [CPW][KMAX][3]) across one workgroup barrier.
+  // Every window's sums are the same operations in the same order as with
+  // WS = 1, so the results are bit-identical.
+  template <int WS = 1>
   static __device__ __forceinline__ void gradient(const double* __restrict__ etab,
                                                   const DT* __restrict__ img, int side,
                                                   const KRStar* tab, double* ftab, int K,
@@ -194,7 +208,8 @@ struct TiledRK {
                                                   const double (&ys)[SLOTS],
                                                   const bool (&own)[SLOTS], const Consts& c,
                                                   const LeanConsts& lc, double (&gf)[SLOTS],
-                                                  double (&gx)[SLOTS], double (&gy)[SLOTS]) {
+                                                  double (&gx)[SLOTS], double (&gy)[SLOTS],
+                                                  int wsub = 0, double* xb = nullptr) {
     const int m = lane_id() & (LPC - 1);
     const int a = m >> 3, b = m & 7;
     const int rmax = side - WR, cmax = side - WC;
@@ -209,9 +224,10 @@ struct TiledRK {
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) {
 #pragma unroll 1
-      for (int kk = 0; kk < LPC; ++kk) {
+      for (int li = 0;; ++li) {  // this wave's windows: kk = wsub + WS li
+        const int kk = wsub + WS * li;
         const int k = LPC * t + kk;
-        if (k >= K) break;
+        if (kk >= LPC || k >= K) break;
         const KRStar sk = tab[k];
         const int R0 = origin(sk.x, WR / 2, rmax), C0 = origin(sk.y, WC / 2, cmax);
         // data pixels of the window (issued before the neighbour work)
@@ -318,13 +334,13 @@ struct TiledRK {
           // every RB windows (and after the slot's last) lane 3 w + c sums row
           // (w, c) over the 32 lanes and lane kk0 + w collects window w's three
           // (ftab is the buffer here)
-          double* row = ftab + (size_t)((kk % RB) * 3) * RP + m;
+          double* row = ftab + (size_t)((li % RB) * 3) * RP + m;
           row[0] = a0;
           row[RP] = fma(dxa, a0, a1);
           row[2 * RP] = fma(dyb, w0, w1);
-          if (kk % RB == RB - 1 || k + 1 == K || kk == LPC - 1) {  // wave-uniform
+          if (li % RB == RB - 1 || k + WS >= K || kk + WS >= LPC) {  // wave-uniform
             wave_lds_sync();
-            const int kk0 = kk - kk % RB;
+            const int li0 = li - li % RB;
             const double* rr = ftab + (size_t)(m < 3 * RB ? m : 0) * RP;
             double v[LPC / 2];  // pairwise tree over the 32 lanes' shares
 #pragma unroll
@@ -334,12 +350,14 @@ struct TiledRK {
 #pragma unroll
               for (int l = 0; l < n; ++l) v[l] = v[l] + v[l + n];
             const double sum = v[0];
-            const int w = m - kk0;                  // this lane's window in the batch
+            // this lane's window in the batch (lane m: star m of the slot)
+            const bool mine = m >= wsub && (m - wsub) % WS == 0;
+            const int w = mine ? (m - wsub) / WS - li0 : -1;
             const int src = (lane_id() & 32) + 3 * (w >= 0 && w < RB ? w : 0);
             const double s0 = __shfl(sum, src, kWave);
             const double s1 = __shfl(sum, src + 1, kWave);
             const double s2 = __shfl(sum, src + 2, kWave);
-            if (w >= 0 && w <= kk - kk0) {
+            if (w >= 0 && w <= li - li0) {
               const double fk = tab[LPC * t + m].f;
               gf[t] = -s0;                          // :404
               gx[t] = -s1 * fk * lc.inv_var;        // :405
@@ -358,6 +376,30 @@ struct TiledRK {
           }
         }
       }
+    }
+    if constexpr (WS > 1) {
+      // the group's swap: lane m publishes its stars evaluated here and reads
+      // the others' (one buffer per gradient, alternating: a barrier between
+      // a buffer's writes and the next writes to it is the next gradient's)
+      double* xc = xb + (size_t)(lane_id() >> 5) * KMAX * 3;  // this chain's rows
+      const bool here = m % WS == wsub;
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t)
+        if (own[t] && here) {
+          double* e = xc + 3 * (LPC * t + m);
+          e[0] = gf[t];
+          e[1] = gx[t];
+          e[2] = gy[t];
+        }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t)
+        if (own[t] && !here) {
+          const double* e = xc + 3 * (LPC * t + m);
+          gf[t] = e[0];
+          gx[t] = e[1];
+          gy[t] = e[2];
+        }
     }
     if (c.use_Vc) {  // repulsion (:411-418), O(K^2) from the star table
 #pragma unroll
@@ -759,10 +801,17 @@ __device__ __forceinline__ bool km_hmc_random_steps(double (&f)[SLOTS], double (
 // SIMD (<= 256 VGPRs) except the fp64-image / K > 32 variant, which needs more.
 // SOLVER: RHMC_SOLVER_IMPLICIT = RHMC_single_step (km_steps), else one of the
 // explicit integrators (km_explicit_steps; f_pos = the flux wall).
-template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT>
+// WS > 1 (implicit solver only: every wave of a workgroup calls the gradient
+// equally often): groups of WS consecutive waves run the same two chains and
+// split their windows (TiledRK::gradient), for launches with too few chains
+// to fill the GPU (C5 split over 8 GPUs: 1024 chains per GPU); group g holds
+// chains 2g, 2g + 1, and waves past the last chain mirror chain 0 rather
+// than leave (the barrier counts them).
+template <typename DT, int SLOTS, bool TAB, int SOLVER = RHMC_SOLVER_IMPLICIT, int WS = 1>
 __global__ void __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(sizeof(DT) == 8 && SLOTS == 2 ? 1 : 2)))
 leapfrog_kr(LeapArgsKR a, int f_pos) {
+  static_assert(WS == 1 || SOLVER == RHMC_SOLVER_IMPLICIT, "window split: implicit steps only");
   using TK = TiledRK<DT, SLOTS, TAB>;
   extern __shared__ double lds[];
   const DT* img;
@@ -778,13 +827,17 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
     img = simg;
   }
   __syncthreads();
-  const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
-  if (TK::CPW * wave >= a.n_chains) return;
+  const int64_t gwave = (int64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x / kWave);
+  const int64_t wave = gwave / WS;      // the chain-pair group
+  const int wsub = (int)(gwave % WS);   // this wave's share of the group's windows
+  if (WS == 1 && TK::CPW * wave >= a.n_chains) return;
   const int lane = lane_id();
   const int h = lane / TK::LPC, m = lane % TK::LPC;
   const int64_t chain = TK::CPW * wave + h;
-  const bool real = chain < a.n_chains;  // ragged tail: mirror the wave's first chain
-  const int64_t chain_r = real ? chain : TK::CPW * wave;
+  // ragged tail: mirror the wave's first chain (a whole group past the end: chain 0)
+  const bool real = chain < a.n_chains && wsub == 0;
+  const int64_t chain_r = chain < a.n_chains ? chain
+                          : (TK::CPW * wave < a.n_chains ? TK::CPW * wave : 0);
   const int64_t cbase = chain_r * 3 * (int64_t)a.K;
   const int W = blockDim.x / kWave;
   const int slot = (threadIdx.x / kWave) * TK::CPW + h;  // chain slot in the workgroup
@@ -792,6 +845,10 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   // TAB: the chain's factor tables; otherwise its deferred-sum buffer
   double* ftab = lds + kExpTab + (size_t)W * TK::CPW * TK::KMAX * (sizeof(KRStar) / 8) +
                  (TAB ? (size_t)slot * a.K * 2 * a.side : (size_t)slot * TK::RED_DOUBLES);
+  // WS > 1: the group's two exchange buffers, after the tables / sum buffers
+  double* xbuf = lds + TK::lds_bytes(W, a.K, a.side) / sizeof(double) +
+                 (size_t)((threadIdx.x / kWave) / WS) * 2 * TK::CPW * TK::KMAX * 3;
+  int xpar = 0;
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
   const int K = a.K;
@@ -815,7 +872,9 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   const int side = a.side;
   auto grad = [&](const double (&xs)[SLOTS], const double (&ys)[SLOTS], double (&gf)[SLOTS],
                   double (&gx)[SLOTS], double (&gy)[SLOTS]) {
-    TK::gradient(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy);
+    TK::template gradient<WS>(lds, img, side, tab, ftab, K, xs, ys, own, c, lc, gf, gx, gy,
+                              wsub, xbuf + (size_t)xpar * TK::CPW * TK::KMAX * 3);
+    xpar ^= 1;
   };
   if constexpr (SOLVER == RHMC_SOLVER_IMPLICIT) {
     km_steps<SLOTS>(f, x, y, pf, px, py, own, tab, a.n_steps, (double)(side - 1), c, lc, grad,

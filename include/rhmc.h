@@ -141,10 +141,16 @@ typedef struct rhmc_ctx rhmc_ctx;
  *                   the LDS factor tables
  * RHMC_OPT_MH_FUSED: 1 (default) = one-launch MH where a fused kernel exists,
  *   0 = the four-kernel loop (begin / leapfrog / energy / end) always.
+ * RHMC_OPT_WINDOW_SPLIT: waves per chain pair in the multi-star
+ *   register-window kernel's implicit step (leapfrog_kr): 0 (default) = by
+ *   batch size (1 from 2 waves per SIMD up, else 2 or 4, so that e.g. C5's
+ *   8192 chains split over 8 GPUs still fill each one), or 1, 2, 4.  The
+ *   results do not depend on it (bit-identical).
  */
 enum {
   RHMC_OPT_KERNEL = 1,
-  RHMC_OPT_MH_FUSED = 2
+  RHMC_OPT_MH_FUSED = 2,
+  RHMC_OPT_WINDOW_SPLIT = 3
 };
 enum {
   RHMC_KERNEL_AUTO = 0,

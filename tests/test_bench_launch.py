@@ -54,13 +54,16 @@ def test_gpus_flag_with_pinned_device():
     assert d["n_gpus"] == 2 and {r["gpu"] for r in d["ranks"]} == {0}
 
 
-def test_c4_global_set_is_split_not_replicated():
-    """C4 = one 2^20-chain set split over the ranks (strong scaling)."""
-    out = _bench(["--gpus", "2", "--dry-run", "--workload", "C4"])
+@pytest.mark.parametrize("wl,total", [("C4", 1 << 20), ("C5", 8192)])
+def test_global_set_is_split_not_replicated(wl, total):
+    """C4 = one 2^20-chain set, C5 one 8192-chain set, split over the ranks
+    (strong scaling, BASELINE configs[3], [4])."""
+    out = _bench(["--gpus", "2", "--dry-run", "--workload", wl])
     assert out.returncode == 0, out.stderr[-3000:]
     d = _line(out)
-    assert d["config"]["total_chains"] == 1 << 20
-    assert sum(r["chains"] for r in d["ranks"]) == 1 << 20
+    assert d["config"]["total_chains"] == total
+    assert sum(r["chains"] for r in d["ranks"]) == total
+    assert d["scaling"] == "strong"
 
 
 def test_gpus_disagreeing_with_world_size_fails():

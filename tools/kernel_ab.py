@@ -19,12 +19,19 @@ ap.add_argument("kernels", nargs="+")
 ap.add_argument("--chains", type=int, default=None)
 ap.add_argument("--reps", type=int, default=3)
 ap.add_argument("--launches", type=int, default=10)
+ap.add_argument("--window-split", type=int, nargs="*", default=[0],
+                help="RHMC_OPT_WINDOW_SPLIT values to alternate (multi-star kernel)")
 args = ap.parse_args()
 wl = workloads.make(args.workload, n_chains=args.chains)
 P = capi.make_params(**wl.params)
 dev = torch.device("cuda:0")
 stream = torch.cuda.Stream(dev)
-ctxs = {k: capi.Context(wl.D, device=0, kernel=k) for k in args.kernels}
+ctxs = {}
+for k in args.kernels:
+    for ws in args.window_split:
+        ctx = capi.Context(wl.D, device=0, kernel=k)
+        ctx.set_option(capi.OPT_WINDOW_SPLIT, ws)
+        ctxs[k if len(args.window_split) == 1 else "%s/ws%d" % (k, ws)] = ctx
 for r in range(args.reps):
     for k, ctx in ctxs.items():
         q = torch.from_numpy(wl.q0).to(dev)
