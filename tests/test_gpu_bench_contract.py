@@ -37,3 +37,24 @@ def test_bench_json_line():
     e = d["end_to_end"]
     assert e["unit"] == d["unit"] and 0 < e["value"] <= 1.05 * d["value"]
     assert d["cpu_baseline"] is None              # --no-cpu
+
+
+@pytest.mark.gpu
+def test_c5_split_over_two_rank_processes_on_one_gpu():
+    """BASELINE configs[4]: C5 is one 8192-chain set split over the ranks.  Two
+    rank processes rehearsed on GPU 0 (RHMC_BENCH_DEVICE) each run a 4096-chain
+    shard; the line reports the global set and strong scaling."""
+    env = dict(os.environ, RHMC_BENCH_DEVICE="0")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, "bench.py", "--workload", "C5", "--gpus", "2",
+                          "--no-cpu", "--no-e2e", "--steps", "1", "--warmup", "0", "--leap", "20"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong"
+    assert d["config"]["total_chains"] == 8192 and d["config"]["chains_per_gpu"] == 4096
+    assert d["config"]["K"] == 64 and d["nonfinite_chains"] == 0
+    assert d["value"] > 0
