@@ -497,8 +497,10 @@ def roofline(pmc, wl, chain_steps, launch_ms):
         "chain_steps_per_launch": chain_steps,
         "executed_fp64_flops_per_chain_step": fpc,
         "valu_active_frac": pmc.get("valu_active_frac"),
+        "simd_valu_issue_frac": pmc.get("simd_valu_issue_frac"),
         "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
-        "pmc_source": ("profiles/pmc_%s.json (%s)" % (wl.name.lower(), pmc.get("kernel", "?"))
+        "pmc_source": ("profiles/pmc_%s.json (%s, revision %s)"
+                       % (wl.name.lower(), pmc.get("kernel", "?"), pmc.get("head", "?"))
                        if pmc else None),
         "hbm_measured_gbs": None if traffic is None else traffic / s / 1e9,
         "hbm_measured_frac": None if traffic is None else traffic / s / 1e9 / HBM_PEAK_GBS,

@@ -49,6 +49,17 @@ if "SQ_ACTIVE_INST_VALU" in avg and "SQ_WAVE_CYCLES" in avg:
     out["valu_active_frac"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_WAVE_CYCLES"]
 if "GRBM_GUI_ACTIVE" in avg:
     out["note_clock"] = "effective clock = GRBM_GUI_ACTIVE / 8 / kernel time"
+    if "SQ_INSTS_VALU" in avg and "SQ_INSTS_VALU_TRANS_F64" in avg:
+        # the SIMDs' VALU issue share: 4 cycles per wave64 VALU instruction plus
+        # ~12 more per v_rcp_f64 (tools/isa_bench.hip), per SIMD (256 CUs x 4),
+        # over the kernel's cycles (GRBM_GUI_ACTIVE summed over the 8 XCDs).
+        # Unlike valu_active_frac it does not depend on the waves per SIMD.
+        kcyc = avg["GRBM_GUI_ACTIVE"] / 8
+        issue = (4 * avg["SQ_INSTS_VALU"] + 12 * avg["SQ_INSTS_VALU_TRANS_F64"]) / 1024
+        out["simd_valu_issue_frac"] = issue / kcyc
+        out["waves_per_simd_resident"] = (avg["SQ_WAVE_CYCLES"] / avg["SQ_BUSY_CYCLES"]) / 7.77
+        out["note_waves"] = ("waves_per_simd_resident: SQ_WAVE_CYCLES / SQ_BUSY_CYCLES "
+                             "normalised by C2's 7.77 (exactly one wave per SIMD)")
 dst = os.path.join("profiles", "pmc_%s.json" % wl)
 with open(dst, "w") as fh:
     json.dump(out, fh, indent=1, sort_keys=True)
