@@ -154,7 +154,9 @@ __device__ __forceinline__ void mh_pk_load(const double* q, const MhPkIds& id, i
   s.x = own ? q[e + 1] : 0.0;
   s.y = own ? q[e + 2] : 0.0;
   s.pad = flux_fold(s.f);
-  tab[id.m] = s;
+  // the table holds PK::NSTAR < 32 entries: lanes K .. NSTAR - 2 write the
+  // placeholder, lanes past them read entry NSTAR - 2 (the last is E0's)
+  if (id.m < PK::NSTAR - 1) tab[id.m] = s;
 }
 
 // Workgroup prologue shared by the two kernels: exp table, image; returns the
@@ -163,7 +165,7 @@ template <class PK, int IMG>
 __device__ __forceinline__ float* mh_pk_stage(double* lds, const float* Df) {
   const int W = blockDim.x / kWave;
   exp_tab_fill(lds);
-  float* simg = reinterpret_cast<float*>(lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
+  float* simg = reinterpret_cast<float*>(lds + kExpTab + PK::star_doubles(W) +
                                          (size_t)W * PK::CPW * PK::tab_doubles());
   for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x)
     simg[PK::img_index(e / IMG, e % IMG)] = Df[e];
@@ -184,8 +186,8 @@ mh_pk_v0(MhKArgs a, double* V) {
       (int64_t)blockIdx.x * W + __builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
   if (PK::CPW * wave >= a.n) return;
   const MhPkIds id = mh_ids<PK::CPW, PK::LPC>(a.n);
-  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::LPC;
-  double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
+  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::NSTAR;
+  double* rtab = lds + kExpTab + PK::star_doubles(W) +
                  (size_t)id.slot * PK::tab_doubles();
   mh_pk_load<PK>(a.q, id, a.K, tab);
   const LeanConsts lc = lean_consts(a.c);
@@ -226,11 +228,11 @@ mh_pk_iter(MhKArgs a, int it, double* V) {
   double f[1], x[1], y[1], pf[1], px[1], py[1];
   {
     const MhPkIds id = mh_ids<PK::CPW, PK::LPC>(a.n);
-    KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::LPC;
+    KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::NSTAR;
     const bool own = id.m < K;
     mh_pk_load<PK>(a.q, id, K, tab);
     wave_lds_sync();
-    const KRStar s0 = tab[id.m];
+    const KRStar s0 = tab[id.m < PK::NSTAR - 2 ? id.m : PK::NSTAR - 2];
     f[0] = s0.f;
     x[0] = s0.x;
     y[0] = s0.y;
@@ -256,7 +258,7 @@ mh_pk_iter(MhKArgs a, int it, double* V) {
     const double V0 = V[id.chr];
     const double T0 = MP::kinetic(f[0], pf[0], px[0], py[0], own, K, c);
     const double E0 = V0 + T0;
-    if (id.m == PK::LPC - 1) tab[PK::LPC - 1].pad = E0;  // entry 31: never a star (K <= 10)
+    if (id.m == PK::LPC - 1) tab[PK::NSTAR - 1].pad = E0;  // the last entry: never a star (K <= KMAX)
     if (id.real) {
       if (a.q_chain && own) {
         a.q_chain[r * d + 3 * id.m] = f[0];
@@ -272,8 +274,8 @@ mh_pk_iter(MhKArgs a, int it, double* V) {
   }
   {
     const MhPkIds id = mh_ids<PK::CPW, PK::LPC>(a.n);
-    KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::LPC;
-    double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
+    KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::NSTAR;
+    double* rtab = lds + kExpTab + PK::star_doubles(W) +
                    (size_t)id.slot * PK::tab_doubles();
     bool own[1];
     own[0] = id.m < K;
@@ -288,11 +290,11 @@ mh_pk_iter(MhKArgs a, int it, double* V) {
   }
   const int64_t n = karg(a.n);
   const MhPkIds id = mh_ids<PK::CPW, PK::LPC>(n);
-  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::LPC;
-  double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
+  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + id.slot * PK::NSTAR;
+  double* rtab = lds + kExpTab + PK::star_doubles(W) +
                  (size_t)id.slot * PK::tab_doubles();
   const bool own = id.m < K;
-  const double E0 = tab[PK::LPC - 1].pad;
+  const double E0 = tab[PK::NSTAR - 1].pad;
   const double V1 = MP::potential(lds, simg, tab, rtab, K, karg(a.f_pos), c, lc);  // tab: q'
   const KRStar s1 = tab[own ? id.m : 0];
   const double dE = (V1 + MP::kinetic(s1.f, pf[0], px[0], py[0], own, K, c)) - E0;

@@ -112,10 +112,18 @@ struct PixK {
   static_assert(CT >= 1 && CT <= 3, "columns per pass");
   // per chain: row table ex [IMG][KMAX], then column table fey [IMG][KMAX]
   static constexpr size_t tab_doubles() { return (size_t)2 * IMG * KMAX; }
-  // LDS: exp table, star tables (32 per chain), factor tables, image (fp32
+  // star table entries per chain: K <= KMAX stars, the last entry is never a
+  // star (the MH kernel keeps E0 there); 16, not 32, so that two 4-wave
+  // workgroups fit one CU's 160 KB at IMG = 48 (two waves per SIMD)
+  static constexpr int NSTAR = 16;
+  static_assert(KMAX < NSTAR, "star table");
+  static constexpr size_t star_doubles(int waves) {
+    return (size_t)waves * CPW * NSTAR * (sizeof(KRStar) / sizeof(double));
+  }
+  // LDS: exp table, star tables (NSTAR per chain), factor tables, image (fp32
   // [IMG][16][NCP]).
   static __host__ __device__ constexpr size_t lds_bytes(int waves) {
-    return kExpTab * sizeof(double) + (size_t)waves * CPW * LPC * sizeof(KRStar) +
+    return kExpTab * sizeof(double) + star_doubles(waves) * sizeof(double) +
            (size_t)waves * CPW * tab_doubles() * sizeof(double) +
            (size_t)IMG * 16 * NCP * sizeof(float);
   }
@@ -358,7 +366,7 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;
   exp_tab_fill(lds);
-  float* simg = reinterpret_cast<float*>(lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 +
+  float* simg = reinterpret_cast<float*>(lds + kExpTab + PK::star_doubles(W) +
                                          (size_t)W * PK::CPW * PK::tab_doubles());
   for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x)
     simg[PK::img_index(e / IMG, e % IMG)] = a.Df[e];
@@ -373,8 +381,8 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   const int64_t chain_r = real ? chain : PK::CPW * wave;
   const int64_t cbase = chain_r * 3 * (int64_t)a.K;
   const int slot = (threadIdx.x / kWave) * PK::CPW + h;
-  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * PK::LPC;
-  double* rtab = lds + kExpTab + (size_t)W * PK::CPW * PK::LPC * 4 + (size_t)slot * PK::tab_doubles();
+  KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * PK::NSTAR;
+  double* rtab = lds + kExpTab + PK::star_doubles(W) + (size_t)slot * PK::tab_doubles();
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
   const int K = a.K;
