@@ -240,17 +240,26 @@ struct TiledRK {
 
         const double r0 = (double)R0, c0 = (double)C0;
         double lam[NPX];
-#pragma unroll
-        for (int p = 0; p < NPX; ++p) lam[p] = c.B;
+        // Lambda = B + the stars' terms; the first star's FMAs take B itself as
+        // the addend (no copies of B into the NPX accumulators: same values)
+        bool started = false;  // wave-uniform
         auto add_star = [&](double fs, const double (&ex)[TR], const double (&ey)[TC]) {
           // f scales the TC column factors (fewer products than the TR rows)
           double fy[TC];
 #pragma unroll
           for (int j = 0; j < TC; ++j) fy[j] = fs * ey[j];
+          if (started) {
 #pragma unroll
-          for (int i = 0; i < TR; ++i)
+            for (int i = 0; i < TR; ++i)
 #pragma unroll
-            for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], lam[i * TC + j]);
+              for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], lam[i * TC + j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < TR; ++i)
+#pragma unroll
+              for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], c.B);
+          }
+          started = true;
         };
         if constexpr (kAll) {
           // Small images (C3): nearly every window overlaps every star, so
@@ -351,8 +360,9 @@ struct TiledRK {
               for (int l = 0; l < n; ++l) v[l] = v[l] + v[l + n];
             const double sum = v[0];
             // this lane's window in the batch (lane m: star m of the slot)
-            const bool mine = m >= wsub && (m - wsub) % WS == 0;
-            const int w = mine ? (m - wsub) / WS - li0 : -1;
+            const int mf = WS > 1 ? lane_id_fresh() & (LPC - 1) : m;
+            const bool mine = mf >= wsub && (mf - wsub) % WS == 0;
+            const int w = mine ? (mf - wsub) / WS - li0 : -1;
             const int src = (lane_id() & 32) + 3 * (w >= 0 && w < RB ? w : 0);
             const double s0 = __shfl(sum, src, kWave);
             const double s1 = __shfl(sum, src + 1, kWave);
@@ -381,12 +391,13 @@ struct TiledRK {
       // the group's swap: lane m publishes its stars evaluated here and reads
       // the others' (one buffer per gradient, alternating: a barrier between
       // a buffer's writes and the next writes to it is the next gradient's)
-      double* xc = xb + (size_t)(lane_id() >> 5) * KMAX * 3;  // this chain's rows
-      const bool here = m % WS == wsub;
+      const int lf = lane_id_fresh(), mf = lf & (LPC - 1);
+      double* xc = xb + (size_t)(lf >> 5) * KMAX * 3;  // this chain's rows
+      const bool here = mf % WS == wsub;
 #pragma unroll
       for (int t = 0; t < SLOTS; ++t)
         if (own[t] && here) {
-          double* e = xc + 3 * (LPC * t + m);
+          double* e = xc + 3 * (LPC * t + mf);
           e[0] = gf[t];
           e[1] = gx[t];
           e[2] = gy[t];
@@ -395,7 +406,7 @@ struct TiledRK {
 #pragma unroll
       for (int t = 0; t < SLOTS; ++t)
         if (own[t] && !here) {
-          const double* e = xc + 3 * (LPC * t + m);
+          const double* e = xc + 3 * (LPC * t + mf);
           gf[t] = e[0];
           gx[t] = e[1];
           gy[t] = e[2];
@@ -834,8 +845,8 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   const int lane = lane_id();
   const int h = lane / TK::LPC, m = lane % TK::LPC;
   const int64_t chain = TK::CPW * wave + h;
-  // ragged tail: mirror the wave's first chain (a whole group past the end: chain 0)
-  const bool real = chain < a.n_chains && wsub == 0;
+  // ragged tail: mirror the wave's first chain (a whole group past the end:
+  // chain 0); only wave 0 of a group writes its real chains (after the loop)
   const int64_t chain_r = chain < a.n_chains ? chain
                           : (TK::CPW * wave < a.n_chains ? TK::CPW * wave : 0);
   const int64_t cbase = chain_r * 3 * (int64_t)a.K;
@@ -896,14 +907,20 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
                                      grad, st);
   }
 
+  // the output indices again from a volatile lane id (held across the step
+  // loop they cost registers the loop needs: the window-split variants spill)
+  const int lo = lane_id_fresh(), mo = lo % TK::LPC;
+  const int64_t chain_o = TK::CPW * wave + lo / TK::LPC;
+  const bool real_o = chain_o < a.n_chains && wsub == 0;
+  const int64_t cbase_o = chain_o * 3 * (int64_t)a.K;
   unsigned nf = 0u;
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
-    if (!own[t] || !real) continue;
+    if (TK::LPC * t + mo >= K || !real_o) continue;
     if (!(isfinite(f[t]) && isfinite(x[t]) && isfinite(y[t]) && isfinite(pf[t]) &&
           isfinite(px[t]) && isfinite(py[t])))
       nf = RHMC_STATUS_NONFINITE;
-    const int64_t e = cbase + 3 * (int64_t)(TK::LPC * t + m);
+    const int64_t e = cbase_o + 3 * (int64_t)(TK::LPC * t + mo);
     a.q[e] = f[t];
     a.q[e + 1] = x[t];
     a.q[e + 2] = y[t];
@@ -914,11 +931,11 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   unsigned all = st | nf;
 #pragma unroll
   for (int d = 16; d >= 1; d >>= 1) all |= (unsigned)__shfl_xor((int)all, d, kWave);
-  if (m == 0 && real) {
-    if (a.status) a.status[chain] = (int32_t)all;
+  if (mo == 0 && real_o) {
+    if (a.status) a.status[chain_o] = (int32_t)all;
     if (a.fp_iters) {
-      a.fp_iters[2 * chain] = it_p;
-      a.fp_iters[2 * chain + 1] = it_q;
+      a.fp_iters[2 * chain_o] = it_p;
+      a.fp_iters[2 * chain_o + 1] = it_q;
     }
   }
 }

@@ -59,6 +59,13 @@ __device__ __forceinline__ bool near_edge(double v, double edge) {
 
 // ---------------------------------------------------------------- lane moves
 __device__ __forceinline__ int lane_id() { return (int)(threadIdx.x & (kWave - 1)); }
+// The lane id by a volatile read: values derived from it are recomputed where
+// used instead of being hoisted out of a step loop and held in VGPRs.
+__device__ __forceinline__ int lane_id_fresh() {
+  int lid;
+  asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
+  return lid;
+}
 
 // Broadcast lane `src` (wave-uniform) of a double to every lane: two
 // v_readlane_b32 into SGPRs, no LDS traffic.
