@@ -12,14 +12,17 @@
 // so the row table holds ex only and the column factors carry f (fey), which
 // serves Lambda and all three sums.  s = D/Lambda - 1.
 // 32 lanes per chain (two chains per wave64): lane m = 16 rh + cg owns image
-// columns cg, cg + 16, ... and rows rh IMG/2 .. rh IMG/2 + IMG/2 - 1.  Per
+// columns cg, cg + 16, ... and rows rh, rh + 2, ..., rh + IMG - 2 (row pass r
+// of the wave covers rows 2r and 2r + 1 of both chains).  Per
 // gradient each chain builds two LDS tables, ex_k(i) [IMG][KMAX] and
 // fey_k(j) [IMG][KMAX] (2 IMG KMAX / 32 exps per lane); a lane then runs its
 // columns CT at a time: fey of its CT columns in registers, each row's ex
 // read once (KMAX/2 ds_read_b128, broadcast to the 16 lanes of a row half)
 // and used for CT pixels, whose data values sit side by side in the LDS image
 // (layout [row][cg][NCP]: one ds_read_b64 per row for a column pair) and
-// share one v_rcp_f64.  The step loop is km_steps (rhmc_tiledrk.hpp).
+// share one v_rcp_f64.  Row passes interleave the row halves (rows 2r, 2r + 1
+// rather than r, r + IMG/2: +1.2 % at C3, profiles/r03_pk_skip/).  The step
+// loop is km_steps (rhmc_tiledrk.hpp).
 #pragma once
 #include "rhmc_tiledrk.hpp"
 
@@ -149,8 +152,8 @@ struct PixK {
         fey[q][k] = ctab[(cg + 16 * (ci0 + q)) * KMAX + k];
         c0[q][k] = c1[q][k] = 0.0;
       }
-    const double* rt = rtab + (size_t)(rh * NR) * KMAX;
-    const float* dp = simg + (rh * NR * 16 + cg) * NCP + ci0;
+    const double* rt = rtab + (size_t)rh * KMAX;          // row 2 r + rh
+    const float* dp = simg + (rh * 16 + cg) * NCP + ci0;
 // rows per loop iteration
 #ifndef RHMC_PK_ROW_UNROLL
 #define RHMC_PK_ROW_UNROLL 4
@@ -159,7 +162,7 @@ struct PixK {
     for (int r = 0; r < NR; ++r) {
       double ex[KMAX];
 #pragma unroll
-      for (int k = 0; k < KMAX; ++k) ex[k] = rt[r * KMAX + k];
+      for (int k = 0; k < KMAX; ++k) ex[k] = rt[2 * r * KMAX + k];
       double l[N], sv[N];
 #pragma unroll
       for (int q = 0; q < N; ++q) {
@@ -168,7 +171,7 @@ struct PixK {
         for (int k = 0; k < KMAX; ++k) l[q] = fma(ex[k], fey[q][k], l[q]);
       }
       if constexpr (N == 3) {  // one reciprocal for the three pixels
-        const float4 d = *reinterpret_cast<const float4*>(dp + r * 16 * NCP);
+        const float4 d = *reinterpret_cast<const float4*>(dp + 2 * r * 16 * NCP);
         const double l01 = l[0] * l[1];
         const double rr = rcp_nr1(l01 * l[2]);
         const double r01 = l[2] * rr;
@@ -176,14 +179,14 @@ struct PixK {
         sv[1] = fma((double)d.y, l[0] * r01, -1.0);
         sv[2] = fma((double)d.z, l01 * rr, -1.0);
       } else if constexpr (N == 2) {  // one reciprocal for the pixel pair
-        const float2 d = *reinterpret_cast<const float2*>(dp + r * 16 * NCP);
+        const float2 d = *reinterpret_cast<const float2*>(dp + 2 * r * 16 * NCP);
         const double rr = rcp_nr1(l[0] * l[1]);
         sv[0] = fma((double)d.x, l[1] * rr, -1.0);  // D/Lambda - 1 (:379)
         sv[1] = fma((double)d.y, l[0] * rr, -1.0);
       } else {
-        sv[0] = fma((double)dp[r * 16 * NCP], rcp_nr1(l[0]), -1.0);
+        sv[0] = fma((double)dp[2 * r * 16 * NCP], rcp_nr1(l[0]), -1.0);
       }
-      const double w = ((double)(rh * NR + r) + 0.5) - kCtr;
+      const double w = ((double)(2 * r + rh) + 0.5) - kCtr;
 #pragma unroll
       for (int q = 0; q < N; ++q) {
         const double t = w * sv[q];
