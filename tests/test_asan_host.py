@@ -1,0 +1,47 @@
+"""Host AddressSanitizer runs of the C-ABI: the library's host code (argument
+checks, host<->device staging, context lifetime, error strings) built with
+-Xarch_host -fsanitize=address and driven by tests/native/capi_asan.cpp
+(`make -C hmc-stellar-toy-model_amd asan`, also run by __graft_entry__.build()).
+Device code is the product's, unsanitised (GPU ASan is not available here).
+ASan aborts the driver on the first heap error, so exit status 0 means every
+check passed with a clean report."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import PKG_DIR, ROOT
+
+BIN = os.path.join(ROOT, "build", "asan", "capi_asan")
+
+
+def _run(mode, leaks):
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=%d:abort_on_error=1" % (1 if leaks else 0)
+    return subprocess.run([BIN, mode], capture_output=True, text=True, env=env, timeout=240)
+
+
+def test_capi_error_paths_under_asan():
+    """No GPU needed: NULL / bad arguments and the no-device path, leak check on."""
+    if not os.path.exists(BIN):
+        if not os.path.exists("/opt/rocm/bin/hipcc"):
+            pytest.skip("hipcc not available to build the ASan driver")
+        subprocess.run(["make", "-C", PKG_DIR, "-j8", "asan"], check=True, capture_output=True)
+    r = _run("cpu", leaks=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capi_asan cpu: ok" in r.stdout
+    assert "AddressSanitizer" not in r.stderr
+
+
+@pytest.mark.gpu
+def test_capi_every_entry_point_under_asan(gpu_lib):
+    """Every entry point on small ragged batches (K = 1 / 3 / 12, all solvers,
+    MH with host and device randoms and records, data generation, image
+    resize, two context lifetimes) with the host code under ASan.  Leak
+    detection is off: the HIP runtime keeps process-lifetime allocations."""
+    if not os.path.exists(BIN):
+        pytest.skip("build/asan/capi_asan not built (make -C hmc-stellar-toy-model_amd asan)")
+    r = _run("gpu", leaks=False)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "capi_asan gpu: ok" in r.stdout
+    assert "AddressSanitizer" not in r.stderr
