@@ -1125,10 +1125,15 @@ int launch_kr_ws(const rhmc_ctx* ctx, const LeapArgsKR& a, int f_pos, hipStream_
 }
 
 // Waves per chain pair for the implicit window-major kernel: the option, or
-// the least of 1, 2, 4 that puts two waves on every SIMD (4 per CU).
+// the least of 1, 2, 4 that gives the launch eight waves per SIMD (four rounds
+// of the kernel's two resident waves: finer rounds even out the waves' unequal
+// neighbour work).  C5 sweep (profiles/r03_ws/, chain-steps/s, WS 1 / 2 / 4):
+// 1024 chains 5.19e6 / 1.01e7 / 1.29e7, 2048 1.03e7 / 1.39e7 / 1.38e7,
+// 4096 1.42e7 / 1.48e7 / 1.48e7, 8192 1.50e7 / 1.53e7 / 1.52e7,
+// 16384 1.58e7 / 1.58e7 / 1.55e7.
 int kr_window_split(const rhmc_ctx* ctx, int64_t n_chains) {
   if (ctx->window_split) return ctx->window_split;
-  const int64_t pairs = (n_chains + 1) / 2, target = 8 * (int64_t)(ctx->n_cu > 0 ? ctx->n_cu : 256);
+  const int64_t pairs = (n_chains + 1) / 2, target = 32 * (int64_t)(ctx->n_cu > 0 ? ctx->n_cu : 256);
   int ws = 1;
   while (ws < 4 && pairs * ws < target) ws *= 2;
   return ws;
