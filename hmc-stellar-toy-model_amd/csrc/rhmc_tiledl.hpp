@@ -43,6 +43,11 @@ namespace rhmc {
 #define RHMC_LANE_QUAD_RCP 1
 #endif
 constexpr bool kQuadRcp = RHMC_LANE_QUAD_RCP;  // A/B knob (tools/variants)
+// PSF factors by recurrence (0: one exp per row and per column)
+#ifndef RHMC_LANE_REC
+#define RHMC_LANE_REC 1
+#endif
+constexpr bool kLaneRec = RHMC_LANE_REC;
 
 template <typename DT>
 struct Vec16;
@@ -92,27 +97,75 @@ struct TiledL {
 
   // The chain's sums of dphidq pixel terms over its window (every lane of the
   // group gets them): s0 = sum psf s, s1 = sum psf s dx, s2 = sum psf s dy.
+  // PSF factors by recurrence (RHMC_LANE_REC; utils.py:475-486 as in
+  // PixK::tables_rec): runs of kRun entries start from two exps,
+  //   e(v) = exp(-c v^2),  g(v) = exp(-c (2 s v + s^2)),  e(v + s) = e(v) g(v),
+  //   g(v + s) = g(v) exp(-2 c s^2)
+  // (s = 1 for the columns, LPC for the lane's rows): 8 exps per chain for the
+  // 28 columns instead of 28, and 4 per row run instead of one per row; each
+  // entry is at most kRun - 1 products from an exp (within ~25 ulp of the
+  // direct exp).  A lane whose window offsets reach rec_vmax (far or NaN
+  // chain) evaluates its factors directly: the choice depends on nothing but
+  // the chain's own state.
+  static constexpr int kRun = 7;
   static __device__ __forceinline__ void partial(const double* __restrict__ etab,
                                                  const V* __restrict__ sv, double f, double x,
                                                  double y, const Consts& c, const LeanConsts& lc,
                                                  double& s0, double& s1, double& s2) {
     const int g = lane_id() % LPC;
     const int r0 = origin(x), c0 = origin(y);
+    const double cc = lc.inv_two_sig2;
+    // ratio of successive row ratios, exp(-2 c LPC^2)
+    const double KR = LPC == 1 ? lc.k_row
+                    : LPC == 4 ? lc.k_col4 : (lc.k_row * lc.k_row) * (lc.k_row * lc.k_row);
+    const double vfirst = ((double)c0 + 0.5) - y, vlast = ((double)(c0 + WIN - 1) + 0.5) - y;
+    const double ufirst = ((double)(r0 + g) + 0.5) - x;
+    const double ulast = ((double)(r0 + g + LPC * (NR - 1)) + 0.5) - x;
+    const bool rec_c = kLaneRec && fabs(vfirst) < lc.rec_vmax && fabs(vlast) < lc.rec_vmax;
+    const bool rec_r = kLaneRec && fabs(ufirst) < lc.rec_vmax && fabs(ulast) < lc.rec_vmax;
     double ey[WIN], ew[WIN];
+    if (rec_c) {
 #pragma unroll
-    for (int j = 0; j < WIN; ++j) {
-      const double v = ((double)(c0 + j) + 0.5) - y;  // exact offsets
-      ey[j] = exp_neg(-(v * v) * lc.inv_two_sig2, etab) * lc.inv_norm;
-      ew[j] = ey[j] * v;
+      for (int j0 = 0; j0 < WIN; j0 += kRun) {
+        const double v = ((double)(c0 + j0) + 0.5) - y;  // exact offsets
+        double e = exp_neg(-(v * v) * cc, etab) * lc.inv_norm;
+        double h = exp_neg(-fma(2.0, v, 1.0) * cc, etab);
+#pragma unroll
+        for (int l = 0; l < kRun && j0 + l < WIN; ++l) {
+          ey[j0 + l] = e;
+          e = e * h;
+          h = h * lc.k_row;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < WIN; ++j) {
+        const double v = ((double)(c0 + j) + 0.5) - y;  // exact offsets
+        ey[j] = exp_neg(-(v * v) * cc, etab) * lc.inv_norm;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < WIN; ++j) ew[j] = ey[j] * (((double)(c0 + j) + 0.5) - y);
     double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+    double er = 0.0, gr = 0.0;  // row run state (rec_r)
 #pragma unroll 2
     for (int t = 0; t < NR; ++t) {
       const int i = g + LPC * t;
       if (WIN % LPC != 0 && i >= WIN) break;
       const V* row = sv + (r0 + i) * PC + c0;
       const double u = ((double)(r0 + i) + 0.5) - x;
-      const double ex = exp_neg(-(u * u) * lc.inv_two_sig2, etab);
+      double ex;
+      if (rec_r) {
+        if (t % kRun == 0) {  // wave-uniform
+          er = exp_neg(-(u * u) * cc, etab);
+          gr = exp_neg(-fma(2.0 * LPC, u, (double)(LPC * LPC)) * cc, etab);
+        }
+        ex = er;
+        er = er * gr;
+        gr = gr * KR;
+      } else {
+        ex = exp_neg(-(u * u) * cc, etab);
+      }
       const double fe = f * ex;
       double R = 0.0, Ry = 0.0;
       auto acc = [&](int j, double q) {
