@@ -9,6 +9,11 @@ factors_rec) against the oracle, through the C-ABI (rhmc_leapfrog):
 * PSF widths on both sides of the recurrence's range guard: FWHM 1.2 px
   (sigma 0.51, rec_vmax 11.6 < the window offsets: direct factors) and
   FWHM 2.5 px (recurrence), with images drawn at that width.
+Both run on the register-window kernel (`auto` at these batch sizes) and on the
+lane-group kernel forced to 1 and 4 lanes per chain, whose runs-of-7
+recurrences (rhmc_tiledl.hpp) fall back per lane: chains 8-11 sit 20-85 px
+outside the image, so some of their window offsets are inside rec_vmax (55.6
+px) and some not.
 Tolerances as tests/test_gpu_parity.py: 1e-9 (q) / 1e-8 (p) relative to
 |value| + 1 after the trajectory, iteration counts exact.
 """
@@ -36,7 +41,12 @@ def _check(capi, D, par, q0, p0, steps, chains=None):
     return q, p, st
 
 
-def test_far_chain_wave_and_edges(gpu_lib, monkeypatch):
+KERNELS = ["auto", "lane1", "lane4"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_far_chain_wave_and_edges(gpu_lib, monkeypatch, kernel):
+    monkeypatch.setattr(gpu_lib, "DEFAULT_KERNEL", kernel)
     wl = workloads.make("C2", n_chains=12)
     q0, p0 = wl.q0.copy(), wl.p0.copy()
     q0[2, 1], q0[2, 2] = 300.0, -250.0     # wave 0: far outside (direct factors)
@@ -44,11 +54,17 @@ def test_far_chain_wave_and_edges(gpu_lib, monkeypatch):
     q0[5, 1], q0[5, 2] = 47.3, 1.2
     q0[6, 1], q0[6, 2] = -0.6, 24.0        # just outside the image
     q0[7, 1], q0[7, 2] = 24.0, 47.9
+    q0[8, 1] = -20.0                       # rows 20.5-47.5 px off: recurrence
+    q0[9, 1] = -40.0                       # rows 40.5-67.5 px off: straddles rec_vmax
+    q0[10, 2] = 85.0                       # columns 37.5-64.5 px off: straddles it
+    q0[11, 1], q0[11, 2] = 70.0, -45.0     # both
     _check(gpu_lib, wl.D, wl.params, q0, p0, 30)
 
 
+@pytest.mark.parametrize("kernel", KERNELS)
 @pytest.mark.parametrize("fwhm", [1.2, 2.5])
-def test_psf_widths_either_side_of_the_range_guard(gpu_lib, monkeypatch, fwhm):
+def test_psf_widths_either_side_of_the_range_guard(gpu_lib, monkeypatch, fwhm, kernel):
+    monkeypatch.setattr(gpu_lib, "DEFAULT_KERNEL", kernel)
     par, ftc = workloads.base_params(dt=0.1)
     par["fwhm_pix"] = fwhm
     rng = np.random.RandomState(int(fwhm * 10))
