@@ -132,15 +132,17 @@ struct TiledRK {
   }
 
   // PSF factors of a star at (xs, ys) on the window with origin (r0, c0):
-  // ex[t] at row r0 + 7a + t, ey[u] at column c0 + b + 8u (carries 1/(2 pi s^2)).
+  // ex[t] at row r0 + 7a + t, ey[u] at column c0 + b + 8u (carries `cscale`:
+  // 1/(2 pi s^2), or f/(2 pi s^2) for a neighbour, whose factors only feed
+  // Lambda — one product per lane before the exchange instead of TC after it).
   static __device__ __forceinline__ void factors(const double* __restrict__ etab, double r0,
                                                  double c0, double xs, double ys, int a, int b,
-                                                 const LeanConsts& lc, double (&ex)[TR],
-                                                 double (&ey)[TC]) {
+                                                 const LeanConsts& lc, double cscale,
+                                                 double (&ex)[TR], double (&ey)[TC]) {
     const double vr = (r0 + ((double)(7 * a + b) + 0.5)) - xs;  // exact offsets
     const double er = exp_neg(-(vr * vr) * lc.inv_two_sig2, etab);
     const double vc = (c0 + ((double)(b + 8 * a) + 0.5)) - ys;
-    const double ec = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * lc.inv_norm;
+    const double ec = exp_neg(-(vc * vc) * lc.inv_two_sig2, etab) * cscale;
     // rows: lane (a, t) of my 8-lane row group; columns: lane (u, b)
     ex[0] = swizzle_d<0x18 | (0 << 5)>(er);
     ex[1] = swizzle_d<0x18 | (1 << 5)>(er);
@@ -188,7 +190,7 @@ struct TiledRK {
 #pragma unroll
       for (int j = 0; j < TC; ++j) ey[j] = tc[8 * j];
     } else {
-      factors(etab, (double)R0, (double)C0, ss.x, ss.y, a, b, lc, ex, ey);
+      factors(etab, (double)R0, (double)C0, ss.x, ss.y, a, b, lc, lc.inv_norm, ex, ey);
     }
   }
 
@@ -243,11 +245,7 @@ struct TiledRK {
         // Lambda = B + the stars' terms; the first star's FMAs take B itself as
         // the addend (no copies of B into the NPX accumulators: same values)
         bool started = false;  // wave-uniform
-        auto add_star = [&](double fs, const double (&ex)[TR], const double (&ey)[TC]) {
-          // f scales the TC column factors (fewer products than the TR rows)
-          double fy[TC];
-#pragma unroll
-          for (int j = 0; j < TC; ++j) fy[j] = fs * ey[j];
+        auto add_scaled = [&](const double (&ex)[TR], const double (&fy)[TC]) {
           if (started) {
 #pragma unroll
             for (int i = 0; i < TR; ++i)
@@ -260,6 +258,13 @@ struct TiledRK {
               for (int j = 0; j < TC; ++j) lam[i * TC + j] = fma(ex[i], fy[j], c.B);
           }
           started = true;
+        };
+        auto add_star = [&](double fs, const double (&ex)[TR], const double (&ey)[TC]) {
+          // f scales the TC column factors (fewer products than the TR rows)
+          double fy[TC];
+#pragma unroll
+          for (int j = 0; j < TC; ++j) fy[j] = fs * ey[j];
+          add_scaled(ex, fy);
         };
         if constexpr (kAll) {
           // Small images (C3): nearly every window overlaps every star, so
@@ -290,8 +295,14 @@ struct TiledRK {
             nbm &= nbm - 1;
             const KRStar ss = tab[s];
             double ex[TR], ey[TC];
-            star_factors(etab, ftab, side, s, ss, R0, C0, a, b, lc, ex, ey);
-            add_star(ss.f, ex, ey);
+            if constexpr (TAB) {
+              star_factors(etab, ftab, side, s, ss, R0, C0, a, b, lc, ex, ey);
+              add_star(ss.f, ex, ey);
+            } else {  // ey = f ey: the flux folded in before the exchange
+              factors(etab, (double)R0, (double)C0, ss.x, ss.y, a, b, lc, ss.f * lc.inv_norm,
+                      ex, ey);
+              add_scaled(ex, ey);
+            }
           }
         }
         double ex[TR], ey[TC];
