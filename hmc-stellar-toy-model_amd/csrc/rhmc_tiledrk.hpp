@@ -281,12 +281,20 @@ struct TiledRK {
             }
           }
         } else {
-          // stars whose windows overlap k's window, union over the two chains
+          // stars whose PSF support reaches k's window (rows R0 .. R0 + WR - 1, columns
+          // C0 .. C0 + WC - 1): every pixel 14 px or more from a star in rows or in
+          // columns gets PSF/peak <= 2^-62 (the window bound, reg_window_ok(28)), so
+          // the star counts when x lies in (R0 - 13.5, R0 + WR + 13.5) and y in
+          // (C0 - 13.5, C0 + WC + 13.5) — and always when x or y is NaN (the reference
+          // spreads it); union over the two chains
+          const double rlo = (double)R0 - 13.5, rhi = (double)(R0 + WR) + 13.5;
+          const double clo = (double)C0 - 13.5, chi = (double)(C0 + WC) + 13.5;
           unsigned long long nbm = 0ull;
 #pragma unroll
           for (int t2 = 0; t2 < SLOTS; ++t2) {
             const int j = LPC * t2 + m;
-            const bool nb = own[t2] && j != k && abs(ro[t2] - R0) < WR && abs(co[t2] - C0) < WC;
+            const bool nb = own[t2] && j != k && !(xs[t2] <= rlo || xs[t2] >= rhi) &&
+                            !(ys[t2] <= clo || ys[t2] >= chi);
             const unsigned long long bl = __builtin_amdgcn_ballot_w64(nb);
             nbm |= (unsigned long long)((unsigned)bl | (unsigned)(bl >> 32)) << (LPC * t2);
           }
