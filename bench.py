@@ -537,7 +537,7 @@ def dry_run(args, wl, world, rank, gpu, total_chains):
     return 0
 
 
-def end_to_end(ctx, P, q, p, wl, leap, reps=3):
+def end_to_end(ctx, P, q, p, wl, leap, reps=10):
     """The host-buffer boundary (rhmc_leapfrog): caller-owned
     host q/p in, H2D + the fused launch + D2H, synchronous — what the drop-in
     RHMC_single_step replacement costs a NumPy caller.  Reported beside
