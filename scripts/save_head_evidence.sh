@@ -38,7 +38,7 @@ txt = f'''Round-3 evidence at HEAD {rev} on one MI355X (gpurun box), `scripts/ro
   every C-ABI entry point, `tests/test_asan_host.py`).
 * `c2_bench.json` — the default `python bench.py` line (C2): {c2['value']:.3g}
   chain-leapfrog-steps/s, kernel {r['kernel_ms']:.3f} ms per 500-step launch (HIP events on the
-  launch stream), roofline valu-fp64 frac {r['frac']:.3f}, end_to_end (host buffers, 3 calls)
+  launch stream), roofline valu-fp64 frac {r['frac']:.3f}, end_to_end (host buffers, {c2['end_to_end']['calls']} calls)
   {c2['end_to_end']['value']:.3g}, CPU baseline {c2['cpu_baseline']['value']:.3g} on 16 cores.
   `c2_kernel_stats.csv`: rocprofv3 `--kernel-trace --stats` of `bench.py --no-cpu`.
 * `c2_bench_2ranks_one_gpu.json` — `RHMC_BENCH_DEVICE=0 bench.py --gpus 2` (both ranks on one
