@@ -347,7 +347,182 @@ __global__ void __launch_bounds__(256) leapfrog_kernel(LeapArgs a) {
   store_chain(a, chain, base, owner, s, it_p, it_q, st);
 }
 
-// Windowed kernel (any square image, 1 <= K <= 64): D from global memory.
+// ---------------------------------------------------------------------------
+// Windowed kernels (rhmc_windowed.hpp): any square image, 1 <= K <= 256, one
+// wave per chain, star 64 s + lane in register slot s (SLOTS = 1, 2, 4).
+template <int SLOTS>
+struct WinState {
+  double f[SLOTS], x[SLOTS], y[SLOTS], pf[SLOTS], px[SLOTS], py[SLOTS];
+  bool own[SLOTS];
+};
+
+// Lanes without a star in a slot carry a copy of star 0 (finite, never read).
+template <int SLOTS>
+__device__ __forceinline__ void win_load(const LeapArgs& a, int64_t chain, int K,
+                                         WinState<SLOTS>& s) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    s.own[t] = kWave * t + lane < K;
+    const int64_t e = chain * 3 * (int64_t)K + 3 * (s.own[t] ? kWave * t + lane : 0);
+    s.f[t] = a.q[e];
+    s.x[t] = a.q[e + 1];
+    s.y[t] = a.q[e + 2];
+    s.pf[t] = a.p[e];
+    s.px[t] = a.p[e + 1];
+    s.py[t] = a.p[e + 2];
+  }
+}
+
+template <int SLOTS>
+__device__ __forceinline__ void win_store(const LeapArgs& a, int64_t chain, int K,
+                                          const WinState<SLOTS>& s, int it_p, int it_q,
+                                          unsigned st) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    if (!s.own[t]) continue;
+    if (!(isfinite(s.f[t]) && isfinite(s.x[t]) && isfinite(s.y[t]) && isfinite(s.pf[t]) &&
+          isfinite(s.px[t]) && isfinite(s.py[t])))
+      st |= RHMC_STATUS_NONFINITE;
+    const int64_t e = chain * 3 * (int64_t)K + 3 * (kWave * t + lane);
+    a.q[e] = s.f[t];
+    a.q[e + 1] = s.x[t];
+    a.q[e + 2] = s.y[t];
+    a.p[e] = s.pf[t];
+    a.p[e + 1] = s.px[t];
+    a.p[e + 2] = s.py[t];
+  }
+  unsigned all = s.own[0] ? st : 0u;  // status bits are only set for owned slots
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) all |= (unsigned)__shfl_xor((int)all, m, kWave);
+  if (lane == 0) {
+    if (a.status) a.status[chain] = (int32_t)all;
+    if (a.fp_iters) {
+      a.fp_iters[2 * chain] = it_p;
+      a.fp_iters[2 * chain + 1] = it_q;
+    }
+  }
+}
+
+// n_steps RHMC_single_step()s (sampler_RHMC.py:522-566) on the slotted state,
+// the reference-form metric of run_steps; the fixed-point tests take np.max
+// over all 3K coordinates (NaN propagates) with one wave max per iteration.
+template <int SLOTS, class Grad>
+__device__ __forceinline__ void run_steps_win(WinState<SLOTS>& s, int n_steps, int rows,
+                                              int cols, const Consts& c, int& it_p, int& it_q,
+                                              unsigned& st, Grad grad) {
+  const double hdt = c.hdt;
+  for (int step = 0;; ++step) {
+    double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+    grad(s.f, s.x, s.y, gf, gx, gy);
+    if (step > 0) {
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        // (5) closing half kick of the previous step (:551), (6) reflection (:554-564)
+        s.pf[t] = s.pf[t] - hdt * gf[t];
+        s.px[t] = s.px[t] - hdt * gx[t];
+        s.py[t] = s.py[t] - hdt * gy[t];
+        unsigned b = 0u;
+        if (s.f[t] < c.f_lim) {
+          s.pf[t] = -s.pf[t];
+          b |= RHMC_STATUS_REFLECT_F;
+          if (s.f[t] >= c.near_f) b |= RHMC_STATUS_NEAR_WALL;
+        }
+        if (s.x[t] < 0.0 || s.x[t] > (double)(rows - 1)) {
+          s.px[t] = -s.px[t];
+          b |= RHMC_STATUS_REFLECT_XY;
+          if (near_edge(s.x[t], (double)(rows - 1))) b |= RHMC_STATUS_NEAR_WALL;
+        }
+        if (s.y[t] < 0.0 || s.y[t] > (double)(cols - 1)) {
+          s.py[t] = -s.py[t];
+          b |= RHMC_STATUS_REFLECT_XY;
+          if (near_edge(s.y[t], (double)(cols - 1))) b |= RHMC_STATUS_NEAR_WALL;
+        }
+        if (s.own[t]) st |= b;
+      }
+    }
+    if (step == n_steps) break;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {  // (1) opening half kick (:525)
+      s.pf[t] = s.pf[t] - hdt * gf[t];
+      s.px[t] = s.px[t] - hdt * gx[t];
+      s.py[t] = s.py[t] - hdt * gy[t];
+    }
+    {  // (2) p fixed point, flux slots only (:528-535); x/y slots change by 0
+      double coef[SLOTS], rho[SLOTS];
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        coef[t] = dtaudq_coef(s.f[t], c);
+        rho[t] = s.pf[t];
+      }
+      double dp;
+      int n = 0;
+      do {
+        double d = 0.0;
+#pragma unroll
+        for (int t = 0; t < SLOTS; ++t) {
+          const double pp = rho[t] - hdt * ((s.pf[t] * s.pf[t]) * coef[t] / 2.0);
+          const double dd = s.own[t] ? fabs(s.pf[t] - pp) : 0.0;
+          d = t == 0 ? dd : nanmax2(d, dd);
+          s.pf[t] = pp;
+        }
+        dp = wave_nanmax(d);
+        ++n;
+      } while (dp > c.delta && n < c.counter_max);
+      it_p += n;
+      if (dp > c.delta) st |= RHMC_STATUS_PLOOP_CAP;
+    }
+    {  // (3) q fixed point (:538-545): q' = sig + dt/2 (p/H(sig) + p/H(q))
+      double sf[SLOTS], sx[SLOTS], sy[SLOTS], af[SLOTS], ax[SLOTS], ay[SLOTS];
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        sf[t] = s.f[t];
+        sx[t] = s.x[t];
+        sy[t] = s.y[t];
+        const double hff0 = H_ff(sf[t], c), hxx0 = H_xx(sf[t], c);
+        af[t] = s.pf[t] / hff0;
+        ax[t] = s.px[t] / hxx0;
+        ay[t] = s.py[t] / hxx0;
+      }
+      double dq;
+      int n = 0;
+      do {
+        double d = 0.0;
+#pragma unroll
+        for (int t = 0; t < SLOTS; ++t) {
+          const double hff = H_ff(s.f[t], c), hxx = H_xx(s.f[t], c);
+          const double nf = sf[t] + hdt * (af[t] + s.pf[t] / hff);
+          const double nx = sx[t] + hdt * (ax[t] + s.px[t] / hxx);
+          const double ny = sy[t] + hdt * (ay[t] + s.py[t] / hxx);
+          double dd =
+              nanmax2(nanmax2(fabs(s.f[t] - nf), fabs(s.x[t] - nx)), fabs(s.y[t] - ny));
+          dd = s.own[t] ? dd : 0.0;
+          d = t == 0 ? dd : nanmax2(d, dd);
+          s.f[t] = nf;
+          s.x[t] = nx;
+          s.y[t] = ny;
+        }
+        dq = wave_nanmax(d);
+        ++n;
+      } while (dq > c.delta && n < c.counter_max);
+      it_q += n;
+      if (dq > c.delta) st |= RHMC_STATUS_QLOOP_CAP;
+    }
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t)  // (4) p -= dt/2 dtaudq(q, p) (:548)
+      s.pf[t] = s.pf[t] - hdt * ((s.pf[t] * s.pf[t]) * dtaudq_coef(s.f[t], c) / 2.0);
+  }
+}
+
+template <int SLOTS>
+__device__ __forceinline__ WinTables win_tables(double* lds, int K) {
+  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+  return WinTables{base_tab, base_tab + K * kTabW};
+}
+
+// Windowed leapfrog (any square image, 1 <= K <= 64 SLOTS): D from global memory.
+template <int SLOTS>
 __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
   extern __shared__ double lds[];
   const Consts& c = a.c;
@@ -355,20 +530,20 @@ __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
-  const bool owner = lane_id() < K;
-  int64_t base;
-  StarState s = load_chain(a, chain, K, owner, base);
+  WinState<SLOTS> s;
+  win_load<SLOTS>(a, chain, K, s);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
   const int rows = a.g.rows, cols = a.g.cols;
-  run_steps<false>(s, owner, a.n_steps, rows, cols, c, it_p, it_q, st,
-                   [&](double f, double x, double y, double& gf, double& gx, double& gy) {
-                     win_gradient(a.D, tab, K, f, x, y, rows, cols, c, lc, true, gf, gx, gy);
-                   });
-  store_chain(a, chain, base, owner, s, it_p, it_q, st);
+  run_steps_win<SLOTS>(
+      s, a.n_steps, rows, cols, c, it_p, it_q, st,
+      [&](const double(&f)[SLOTS], const double(&x)[SLOTS], const double(&y)[SLOTS],
+          double(&gf)[SLOTS], double(&gx)[SLOTS], double(&gy)[SLOTS]) {
+        win_gradient<SLOTS>(a.D, tab, K, f, x, y, rows, cols, c, lc, true, gf, gx, gy);
+      });
+  win_store<SLOTS>(a, chain, K, s, it_p, it_q, st);
 }
 
 struct GradArgs {
@@ -512,7 +687,7 @@ __device__ __forceinline__ double dVdq_rhmc_f(double f, double pf, const Consts&
   return (t1 + t2) / 2.0;
 }
 
-template <int SOLVER>
+template <int SOLVER, int SLOTS>
 __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_pos) {
   extern __shared__ double lds[];
   const Consts& c = a.c;
@@ -520,61 +695,85 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
-  const bool owner = lane_id() < K;
-  int64_t base;
-  StarState s = load_chain(a, chain, K, owner, base);
+  WinState<SLOTS> s;
+  win_load<SLOTS>(a, chain, K, s);
   const int rows = a.g.rows, cols = a.g.cols;
   const double dt = c.dt;
   unsigned st = 0u;
-  double gf, gx, gy;
-  win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-  for (int step = 0; step < a.n_steps; ++step) {
-    if (SOLVER == RHMC_SOLVER_HMC) {
-      const double hf = s.pf - dt * gf / 2.0, hx = s.px - dt * gx / 2.0, hy = s.py - dt * gy / 2.0;
-      s.f = s.f + dt * hf;
-      s.x = s.x + dt * hx;
-      s.y = s.y + dt * hy;
-      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-      s.pf = hf - dt * gf / 2.0;
-      s.px = hx - dt * gx / 2.0;
-      s.py = hy - dt * gy / 2.0;
-    } else if (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {
-      const double hff = H_ff(s.f, c), hxx = H_xx(s.f, c);
-      const double nf = s.f + dt * s.pf / hff, nx = s.x + dt * s.px / hxx,
-                   ny = s.y + dt * s.py / hxx;
-      const double pf_old = s.pf;
-      s.pf = s.pf - dt * (gf + dVdq_rhmc_f(s.f, s.pf, c));
-      s.px = s.px - dt * (gx + 0.0);
-      s.py = s.py - dt * (gy + 0.0);
-      if (f_pos && nf < c.f_lim) {
-        s.pf = pf_old * -1.0;
-        st |= RHMC_STATUS_REFLECT_F;
+  double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+  // One gradient call site (the gradient is most of the kernel: a second
+  // copy is not inlined and its array arguments go to scratch).  Pass `step`
+  // closes step - 1 and opens step; the gradient at the end of a step is the
+  // next step's first one (same q).
+  for (int step = 0;; ++step) {
+    if (SOLVER == RHMC_SOLVER_RHMC_NAIVE && step == a.n_steps) break;
+    win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+    if (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :690-708, the gradient at the step's start
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        const double hff = H_ff(s.f[t], c), hxx = H_xx(s.f[t], c);
+        const double nf = s.f[t] + dt * s.pf[t] / hff, nx = s.x[t] + dt * s.px[t] / hxx,
+                     ny = s.y[t] + dt * s.py[t] / hxx;
+        const double pf_old = s.pf[t];
+        s.pf[t] = s.pf[t] - dt * (gf[t] + dVdq_rhmc_f(s.f[t], s.pf[t], c));
+        s.px[t] = s.px[t] - dt * (gx[t] + 0.0);
+        s.py[t] = s.py[t] - dt * (gy[t] + 0.0);
+        if (f_pos && nf < c.f_lim) {
+          s.pf[t] = pf_old * -1.0;
+          if (s.own[t]) st |= RHMC_STATUS_REFLECT_F;
+        }
+        s.f[t] = nf;
+        s.x[t] = nx;
+        s.y[t] = ny;
       }
-      s.f = nf;
-      s.x = nx;
-      s.y = ny;
-      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-    } else {  // RHMC_SOLVER_RHMC_LEAPFROG
-      const double hff = H_ff(s.f, c), hxx = H_xx(s.f, c);
-      const double hf = s.pf - dt * (gf + dVdq_rhmc_f(s.f, s.pf, c)) / 2.0;
-      const double hx = s.px - dt * (gx + 0.0) / 2.0, hy = s.py - dt * (gy + 0.0) / 2.0;
-      s.f = s.f + dt * hf / hff;
-      s.x = s.x + dt * hx / hxx;
-      s.y = s.y + dt * hy / hxx;
-      win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-      s.pf = hf - dt * (gf + dVdq_rhmc_f(s.f, hf, c)) / 2.0;
-      s.px = hx - dt * (gx + 0.0) / 2.0;
-      s.py = hy - dt * (gy + 0.0) / 2.0;
-      if (f_pos && s.f < c.f_lim) {
-        s.pf = hf * -1.0;
-        st |= RHMC_STATUS_REFLECT_F;
+      continue;
+    }
+    if (step > 0) {  // second half kick of step - 1 (p holds the half-step momentum)
+#pragma unroll
+      for (int t = 0; t < SLOTS; ++t) {
+        if (SOLVER == RHMC_SOLVER_HMC) {  // :628-638
+          s.pf[t] = s.pf[t] - dt * gf[t] / 2.0;
+        } else {                          // :709-728
+          const double hf = s.pf[t];
+          s.pf[t] = hf - dt * (gf[t] + dVdq_rhmc_f(s.f[t], hf, c)) / 2.0;
+          if (f_pos && s.f[t] < c.f_lim) {
+            s.pf[t] = hf * -1.0;
+            if (s.own[t]) st |= RHMC_STATUS_REFLECT_F;
+          }
+        }
+        s.px[t] = s.px[t] - dt * (gx[t] + 0.0) / 2.0;
+        s.py[t] = s.py[t] - dt * (gy[t] + 0.0) / 2.0;
+      }
+    }
+    if (step == a.n_steps) break;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {  // first half kick and drift of step
+      if (SOLVER == RHMC_SOLVER_HMC) {
+        const double hf = s.pf[t] - dt * gf[t] / 2.0, hx = s.px[t] - dt * gx[t] / 2.0,
+                     hy = s.py[t] - dt * gy[t] / 2.0;
+        s.f[t] = s.f[t] + dt * hf;
+        s.x[t] = s.x[t] + dt * hx;
+        s.y[t] = s.y[t] + dt * hy;
+        s.pf[t] = hf;
+        s.px[t] = hx;
+        s.py[t] = hy;
+      } else {
+        const double hff = H_ff(s.f[t], c), hxx = H_xx(s.f[t], c);
+        const double hf = s.pf[t] - dt * (gf[t] + dVdq_rhmc_f(s.f[t], s.pf[t], c)) / 2.0;
+        const double hx = s.px[t] - dt * (gx[t] + 0.0) / 2.0,
+                     hy = s.py[t] - dt * (gy[t] + 0.0) / 2.0;
+        s.f[t] = s.f[t] + dt * hf / hff;
+        s.x[t] = s.x[t] + dt * hx / hxx;
+        s.y[t] = s.y[t] + dt * hy / hxx;
+        s.pf[t] = hf;
+        s.px[t] = hx;
+        s.py[t] = hy;
       }
     }
   }
-  store_chain(a, chain, base, owner, s, 0, 0, st);
+  win_store<SLOTS>(a, chain, K, s, 0, 0, st);
 }
 
 // samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552):
@@ -585,7 +784,8 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
 // every later step in which ANY star is below it, :529-541), and when the
 // last step flipped, p_tmp keeps the momentum the trajectory started from
 // (:547-550 update p_half, not p_tmp) — status bit RHMC_STATUS_REFLECT_F
-// marks those chains.  One wave per chain, lane k < K owns star k.
+// marks those chains.  One wave per chain, star 64 s + lane in slot s.
+template <int SLOTS>
 __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
                                                              const double* __restrict__ dtv,
                                                              const int32_t* __restrict__ steps) {
@@ -595,72 +795,111 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
   const int lane = lane_id();
-  const bool owner = lane < K;
-  int64_t base;
-  StarState s = load_chain(a, chain, K, owner, base);
+  WinState<SLOTS> s;
+  win_load<SLOTS>(a, chain, K, s);
   const int rows = a.g.rows, cols = a.g.cols;
-  const int ks = owner ? lane : 0;
-  const double dtf = dtv[3 * ks], dtx = dtv[3 * ks + 1], dty = dtv[3 * ks + 2];
-  double gf, gx, gy;
-  win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-  double hf = s.pf - dtf * gf / 2.0, hx = s.px - dtx * gx / 2.0,  // :519
-         hy = s.py - dty * gy / 2.0;
-  bool iflip = false, flip = false;
+  double dtf[SLOTS], dtx[SLOTS], dty[SLOTS];
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    const int ks = s.own[t] ? kWave * t + lane : 0;
+    dtf[t] = dtv[3 * ks];
+    dtx[t] = dtv[3 * ks + 1];
+    dty[t] = dtv[3 * ks + 2];
+  }
+  double gf[SLOTS], gx[SLOTS], gy[SLOTS];
+  win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+  double hf[SLOTS], hx[SLOTS], hy[SLOTS];
+  bool iflip[SLOTS];
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {  // :519
+    hf[t] = s.pf[t] - dtf[t] * gf[t] / 2.0;
+    hx[t] = s.px[t] - dtx[t] * gx[t] / 2.0;
+    hy[t] = s.py[t] - dty[t] * gy[t] / 2.0;
+    iflip[t] = false;
+  }
+  bool flip = false;
   const int n = steps[chain];
-  for (int t = 0; t < n; ++t) {
-    s.f = s.f + dtf * hf;                                             // :523
-    s.x = s.x + dtx * hx;
-    s.y = s.y + dty * hy;
-    const bool below = owner && s.f < c.f_lim;                        // :526-529
-    iflip = iflip || below;
-    flip = __builtin_amdgcn_ballot_w64(below) != 0;
-    win_gradient(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
-    const double kept = -hf;                                          // :531
-    hf = hf - dtf * gf;                                               // :532, :535
-    hx = hx - dtx * gx;
-    hy = hy - dty * gy;
-    if (flip && iflip) hf = kept;                                     // :533
+  for (int i = 0; i < n; ++i) {
+    bool below_any = false;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      s.f[t] = s.f[t] + dtf[t] * hf[t];                                 // :523
+      s.x[t] = s.x[t] + dtx[t] * hx[t];
+      s.y[t] = s.y[t] + dty[t] * hy[t];
+      const bool below = s.own[t] && s.f[t] < c.f_lim;                  // :526-529
+      iflip[t] = iflip[t] || below;
+      below_any = below_any || below;
+    }
+    flip = __builtin_amdgcn_ballot_w64(below_any) != 0;
+    win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      const double kept = -hf[t];                                       // :531
+      hf[t] = hf[t] - dtf[t] * gf[t];                                   // :532, :535
+      hx[t] = hx[t] - dtx[t] * gx[t];
+      hy[t] = hy[t] - dty[t] * gy[t];
+      if (flip && iflip[t]) hf[t] = kept;                               // :533
+    }
   }
   unsigned st = 0u;
   if (flip) {
     st |= RHMC_STATUS_REFLECT_F;  // p_tmp stays the starting momentum (:547-550)
   } else {                        // :551-552, dVdq at the same q as the last step
-    s.pf = hf + dtf * gf / 2.0;
-    s.px = hx + dtx * gx / 2.0;
-    s.py = hy + dty * gy / 2.0;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      s.pf[t] = hf[t] + dtf[t] * gf[t] / 2.0;
+      s.px[t] = hx[t] + dtx[t] * gx[t] / 2.0;
+      s.py[t] = hy[t] + dty[t] * gy[t] / 2.0;
+    }
   }
-  store_chain(a, chain, base, owner, s, 0, 0, st);
+  win_store<SLOTS>(a, chain, K, s, 0, 0, st);
+}
+
+// Star 64 t + lane's (f, x, y) of a chain (lanes without a star: star 0's).
+template <int SLOTS>
+__device__ __forceinline__ void win_load_q(const double* q, int64_t chain, int K,
+                                           double (&f)[SLOTS], double (&x)[SLOTS],
+                                           double (&y)[SLOTS], bool (&own)[SLOTS]) {
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    own[t] = win_own(t, K);
+    const int64_t e = chain * 3 * (int64_t)K + 3 * (own[t] ? kWave * t + lane_id() : 0);
+    f[t] = q[e];
+    x[t] = q[e + 1];
+    y[t] = q[e + 2];
+  }
 }
 
 // Large-image gradient (windowed), one wave per chain.
+template <int SLOTS>
 __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
-  const int lane = lane_id();
   const int K = a.K;
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(a.c);
-  const bool owner = lane < K;
-  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
-  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
-  double gf, gx, gy;
-  win_gradient(a.D, tab, K, f, x, y, a.g.rows, a.g.cols, a.c, lc, a.with_metric != 0, gf, gx,
-               gy);
-  if (owner) {
-    a.grad[base] = gf;
-    a.grad[base + 1] = gx;
-    a.grad[base + 2] = gy;
+  double f[SLOTS], x[SLOTS], y[SLOTS], gf[SLOTS], gx[SLOTS], gy[SLOTS];
+  bool own[SLOTS];
+  win_load_q<SLOTS>(a.q, chain, K, f, x, y, own);
+  win_gradient<SLOTS>(a.D, tab, K, f, x, y, a.g.rows, a.g.cols, a.c, lc, a.with_metric != 0,
+                      gf, gx, gy);
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    if (!own[t]) continue;
+    const int64_t e = chain * 3 * (int64_t)K + 3 * (kWave * t + lane_id());
+    a.grad[e] = gf[t];
+    a.grad[e + 1] = gx[t];
+    a.grad[e + 2] = gy[t];
   }
 }
 
 // Large-image V and T (windowed tables, pixel-major V).
+template <int SLOTS>
 __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   extern __shared__ double lds[];
   const Geometry& g = a.g;
@@ -670,19 +909,21 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   if (chain >= a.n_chains) return;
   const int lane = lane_id();
   const int K = a.K;
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  const WinTables tab{base_tab, base_tab + K * kTabW};
+  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
-  const bool owner = lane < K;
-  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
-  const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
+  double f[SLOTS], x[SLOTS], y[SLOTS];
+  bool own[SLOTS];
+  win_load_q<SLOTS>(a.q, chain, K, f, x, y, own);
   if (a.T) {
     double t1 = 0.0, t2 = 0.0;
-    if (owner) {
-      const double pf = a.p[base], px = a.p[base + 1], py = a.p[base + 2];
-      const double hff = H_ff(f, c), hxx = H_xx(f, c);
-      t1 = pf * pf / hff + px * px / hxx + py * py / hxx;
-      t2 = log(fabs(hff)) + log(fabs(hxx)) + log(fabs(hxx));
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      if (!own[t]) continue;
+      const int64_t e = chain * 3 * (int64_t)K + 3 * (kWave * t + lane);
+      const double pf = a.p[e], px = a.p[e + 1], py = a.p[e + 2];
+      const double hff = H_ff(f[t], c), hxx = H_xx(f[t], c);
+      t1 += pf * pf / hff + px * px / hxx + py * py / hxx;
+      t2 += log(fabs(hff)) + log(fabs(hxx)) + log(fabs(hxx));
     }
     t1 = wave_sum(t1);
     t2 = wave_sum(t2);
@@ -690,27 +931,44 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   }
   if (!a.V) return;
   bool bad = false;
-  if (owner) {
-    if ((a.f_pos & RHMC_V_FLUX_WALL) && f < c.f_lim) bad = true;
+#pragma unroll
+  for (int t = 0; t < SLOTS; ++t) {
+    if (!own[t]) continue;
+    if ((a.f_pos & RHMC_V_FLUX_WALL) && f[t] < c.f_lim) bad = true;
     if (!(a.f_pos & RHMC_V_NO_POSCHECK) &&
-        (x < -1.0 || x > (double)(g.rows + 1) || y < -1.0 || y > (double)(g.cols + 1)))
+        (x[t] < -1.0 || x[t] > (double)(g.rows + 1) || y[t] < -1.0 ||
+         y[t] > (double)(g.cols + 1)))
       bad = true;
   }
   if (__any(bad)) {
     if (lane == 0) a.V[chain] = INFINITY;
     return;
   }
-  double v = win_potential(a.D, tab, K, f, x, y, g.rows, g.cols, c, lc);
-  if (c.use_prior) v += wave_sum(owner ? c.alpha * log(f) + c.vprior : 0.0);
-  if (c.use_Vc) {
-    double s = 0.0;
-    for (int jj = 0; jj < K; ++jj) {
-      const double X = bcast(x, jj), Y = bcast(y, jj);
-      double R = sqrt((X - x) * (X - x) + (Y - y) * (Y - y));
-      if (fabs(R) < 1e-10) R = 1e32;
-      s += pow(1.0 / R, c.vc_pow);
+  double v = win_potential<SLOTS>(a.D, tab, K, f, x, y, g.rows, g.cols, c, lc);
+  if (c.use_prior) {
+    double vp = 0.0;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t)
+      if (own[t]) vp += c.alpha * log(f[t]) + c.vprior;
+    v += wave_sum(vp);
+  }
+  if (c.use_Vc) {  // 0.5 beta sum_{a,b} R_ab^-pow with R_aa -> 1e32 (:332-349)
+    double sl = 0.0;
+#pragma unroll
+    for (int t = 0; t < SLOTS; ++t) {
+      double sv = 0.0;
+#pragma unroll
+      for (int t2 = 0; t2 < SLOTS; ++t2) {
+        for (int jl = 0; jl < kWave && kWave * t2 + jl < K; ++jl) {
+          const double X = bcast(x[t2], jl), Y = bcast(y[t2], jl);
+          double R = sqrt((X - x[t]) * (X - x[t]) + (Y - y[t]) * (Y - y[t]));
+          if (fabs(R) < 1e-10) R = 1e32;
+          sv += pow(1.0 / R, c.vc_pow);
+        }
+      }
+      if (own[t]) sl += sv;
     }
-    v += 0.5 * c.beta * wave_sum(owner ? s : 0.0);
+    v += 0.5 * c.beta * wave_sum(sl);
   }
   if (lane == 0) a.V[chain] = v;
 }
@@ -779,7 +1037,23 @@ int window_unsupported() {
 
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
-constexpr int kMaxK = 64;          // windowed kernel: lanes = stars
+constexpr int kMaxK = 256;         // windowed kernels: 64 lanes x 4 star slots
+
+// Star slots per lane of the windowed kernels for K stars.
+int win_slots(int K) { return K <= 64 ? 1 : (K <= 128 ? 2 : 4); }
+
+template <int SLOTS>
+void launch_integrate_win(int32_t solver, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                          const LeapArgs& a, int fp) {
+  if (solver == RHMC_SOLVER_HMC)
+    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_HMC, SLOTS>), grid, block, lds, s, a, fp);
+  else if (solver == RHMC_SOLVER_RHMC_NAIVE)
+    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_RHMC_NAIVE, SLOTS>), grid, block, lds, s,
+                       a, fp);
+  else
+    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_RHMC_LEAPFROG, SLOTS>), grid, block, lds,
+                       s, a, fp);
+}
 
 // Which kernel family serves (K, image): the LDS-image kernels need D and the
 // per-wave tables in LDS and K <= 16; everything else goes windowed.
@@ -796,7 +1070,7 @@ void pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
   int w = 4;
   while (w > 1 && w * per > (size_t)ctx->max_lds) w >>= 1;
   *W = w;
-  *lds = w * per;
+  *lds = w * per;  // K <= 256: 135 KB for one wave, within the CU's 160 KB
 }
 
 Geometry make_geometry(int rows, int cols) {
@@ -886,7 +1160,7 @@ int check_common(rhmc_ctx* ctx, int64_t n_chains, int32_t K) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
   if (n_chains < 0) return fail(RHMC_ERR_ARG, "n_chains < 0");
-  if (K < 1 || K > kMaxK) return fail(RHMC_ERR_ARG, "K must be in [1, 64]");
+  if (K < 1 || K > kMaxK) return fail(RHMC_ERR_ARG, "K must be in [1, 256]");
   if (n_chains > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "n_chains too large");
   return RHMC_OK;
 }
@@ -1087,7 +1361,11 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
-    hipLaunchKernelGGL(energy_win_kernel, grid, block, lds, s, a);
+    switch (win_slots(K)) {
+      case 1: hipLaunchKernelGGL(energy_win_kernel<1>, grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL(energy_win_kernel<2>, grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL(energy_win_kernel<4>, grid, block, lds, s, a); break;
+    }
     HIP_TRY(hipGetLastError());
     return RHMC_OK;
   }
@@ -1286,7 +1564,11 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.n_steps = n_steps;
     pick_waves_win(ctx, K, &lds, &W);
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
-    hipLaunchKernelGGL(leapfrog_win_kernel, grid, block, lds, s, a);
+    switch (win_slots(K)) {
+      case 1: hipLaunchKernelGGL(leapfrog_win_kernel<1>, grid, block, lds, s, a); break;
+      case 2: hipLaunchKernelGGL(leapfrog_win_kernel<2>, grid, block, lds, s, a); break;
+      default: hipLaunchKernelGGL(leapfrog_win_kernel<4>, grid, block, lds, s, a); break;
+    }
     HIP_TRY(hipGetLastError());
     return RHMC_OK;
   }
@@ -1597,13 +1879,11 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
-  if (solver == RHMC_SOLVER_HMC)
-    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_HMC>, grid, block, lds, s, a, fp);
-  else if (solver == RHMC_SOLVER_RHMC_NAIVE)
-    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_RHMC_NAIVE>, grid, block, lds, s, a, fp);
-  else
-    hipLaunchKernelGGL(integrate_win_kernel<RHMC_SOLVER_RHMC_LEAPFROG>, grid, block, lds, s, a,
-                       fp);
+  switch (win_slots(K)) {
+    case 1: launch_integrate_win<1>(solver, grid, block, lds, s, a, fp); break;
+    case 2: launch_integrate_win<2>(solver, grid, block, lds, s, a, fp); break;
+    default: launch_integrate_win<4>(solver, grid, block, lds, s, a, fp); break;
+  }
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -1699,7 +1979,11 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   pick_waves_win(ctx, K, &lds, &W);
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL(hmc_random_win_kernel, grid, block, lds, s, a, d_dt, d_steps);
+  switch (win_slots(K)) {
+    case 1: hipLaunchKernelGGL(hmc_random_win_kernel<1>, grid, block, lds, s, a, d_dt, d_steps); break;
+    case 2: hipLaunchKernelGGL(hmc_random_win_kernel<2>, grid, block, lds, s, a, d_dt, d_steps); break;
+    default: hipLaunchKernelGGL(hmc_random_win_kernel<4>, grid, block, lds, s, a, d_dt, d_steps); break;
+  }
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -1974,7 +2258,11 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
-    hipLaunchKernelGGL(gradient_win_kernel, grid, block, lds, ctx->stream, a);
+    switch (win_slots(K)) {
+      case 1: hipLaunchKernelGGL(gradient_win_kernel<1>, grid, block, lds, ctx->stream, a); break;
+      case 2: hipLaunchKernelGGL(gradient_win_kernel<2>, grid, block, lds, ctx->stream, a); break;
+      default: hipLaunchKernelGGL(gradient_win_kernel<4>, grid, block, lds, ctx->stream, a); break;
+    }
     HIP_TRY(hipGetLastError());
   } else if ((rc = dispatch_k<GradLaunch>(K, grid, block, lds, ctx->stream, a))) {
     return rc;

@@ -864,10 +864,16 @@ leapfrog_kr(LeapArgsKR a, int f_pos) {
   const int lane = lane_id();
   const int h = lane / TK::LPC, m = lane % TK::LPC;
   const int64_t chain = TK::CPW * wave + h;
-  // ragged tail: mirror the wave's first chain (a whole group past the end:
-  // chain 0); only wave 0 of a group writes its real chains (after the loop)
-  const int64_t chain_r = chain < a.n_chains ? chain
-                          : (TK::CPW * wave < a.n_chains ? TK::CPW * wave : 0);
+  // ragged tail: mirror the wave's first chain; a whole group past the end
+  // mirrors the first chain of its own workgroup (never past the end: the
+  // workgroup's first group is real), whose write after the step loop the
+  // workgroup's barriers order after this read; only wave 0 of a group writes
+  // its real chains (after the loop)
+  const int64_t chain_r =
+      chain < a.n_chains ? chain
+      : (TK::CPW * wave < a.n_chains
+             ? TK::CPW * wave
+             : TK::CPW * ((int64_t)blockIdx.x * (blockDim.x / kWave) / WS));
   const int64_t cbase = chain_r * 3 * (int64_t)a.K;
   const int W = blockDim.x / kWave;
   const int slot = (threadIdx.x / kWave) * TK::CPW + h;  // chain slot in the workgroup

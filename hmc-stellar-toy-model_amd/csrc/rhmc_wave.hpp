@@ -39,7 +39,8 @@ struct Consts {
 // flux sum by f again).  At f = 0 that gives 0/0 where the reference's
 // -sum psf (D/Lambda - 1) (:404) is finite, and a subnormal f underflows.  The
 // fold is f pushed 2^-600 away from zero: copysign(|f| + 2^-600, f).  For
-// |f| >= 2^-547 that IS f (2^-600 is below half its ulp), so every ordinary
+// |f| >= 2^-546 that IS f (2^-600 is below half its ulp; in [2^-547, 2^-546)
+// it is exactly half an ulp and rounds an odd mantissa up), so every ordinary
 // chain is bit-identical; for smaller |f| (0 included) the flux sum comes
 // back exactly by the division and Lambda still rounds to B as with f psf.
 // The x, y sums then carry the fold for f: they differ from the reference's

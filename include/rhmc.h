@@ -145,7 +145,11 @@ typedef struct rhmc_ctx rhmc_ctx;
  *   register-window kernel's implicit step (leapfrog_kr): 0 (default) = by
  *   batch size (1 from 2 waves per SIMD up, else 2 or 4, so that e.g. C5's
  *   8192 chains split over 8 GPUs still fill each one), or 1, 2, 4.  The
- *   results do not depend on it (bit-identical).
+ *   results do not depend on it (bit-identical).  It applies only where that
+ *   kernel runs the implicit step without LDS factor tables (images larger
+ *   than 64 px, or K > 16); the factor-table variant, the explicit solvers,
+ *   HMC_random and every other kernel family ignore it, and
+ *   rhmc_ctx_get_option returns the value set either way.
  */
 enum {
   RHMC_OPT_KERNEL = 1,

@@ -339,11 +339,81 @@ def case_trajs(S, U):
     cases["traj_cmax"] = traj_case(
         S, U, 48, [[16., 24.2, 23.9]], lambda g, c: [[16.5, 24.6, 23.3]],
         dict(dt=0.3), 2, 100, cmax=2, delta=1e-9)
-    # C5 geometry: 256x256 K=64, prior, big-sim4 parameters, 3 steps, 1 chain
-    cases["traj_c5"] = traj_case(
+    cases.update(case_c5(S, U))
+    return cases
+
+
+def case_c5(S, U):
+    """C5 geometry (256x256, K = 64, prior, big-sim4 parameters,
+    RHMC-big-sim4.py:11-47): 4 chains x 50 reference steps.  Power-law
+    magnitudes reach 23.3, below the flux wall (f_lim = mag 23), so every
+    chain's flux-wall reflection (sampler_RHMC.py:554-559) fires within these
+    steps; the generator checks that it does."""
+    out = traj_case(
         S, U, 256, lambda g: powlaw_stars(U, g, 64, 256),
         lambda g, c: powlaw_stars(U, g, 64, 256),
-        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True), 1, 3)
+        dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True), 4, 50)
+    f_lim = out["par_f_lim"]
+    refl = (out["Q"][:, 1:, 0::3] < f_lim).any(axis=(1, 2))
+    assert refl.all(), "a C5 chain never reflected at the flux wall: %s" % refl
+    return {"traj_c5": out}
+
+
+def case_bigk(S, U):
+    """K > 64 stars per chain, the reference's own many-star drivers:
+    RHMC-big-sim3.py (32x32, K = 100, prior, repulsion) and RHMC-big-sim4.py
+    (32x32, big-sim4 parameters, births up to N_max = 120, :77).  The
+    reference's dVdq / V / RHMC_single_step are vectorised over any K
+    (sampler_RHMC.py:365-425, :294-351, :522-566).
+
+    bigk.npz: per-function vectors (dVdq, dphidq, V, T, H) at K = 100 (32 px,
+    big-sim4 parameters + prior; and + repulsion Vc_r_pow = 4 as in big-sim3),
+    K = 120 (48 px) and K = 128 (256 px, prior).
+    traj_bigk.npz: 2 chains x 50 steps at 32x32, K = 100 (big-sim4
+    parameters, prior).  traj_bigk256.npz: 1 chain x 4 steps at 256x256,
+    K = 128, prior."""
+    out = {}
+    rs = np.random.RandomState(8)
+    sets = [("b100", 32, 100, None), ("b100vc", 32, 100, (1e-3, 4.)), ("b120", 48, 120, None),
+            ("b128", 256, 128, None)]
+    for name, n, K, vc in sets:
+        np.random.seed(77)
+        g = make_gym(S, n=n, g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True)
+        stars = powlaw_stars(U, g, K, n)
+        if vc is not None:
+            g.use_Vc = True
+            g.beta, g.Vc_r_pow = vc
+            g.f_expnt = np.zeros(K)
+        g.gen_mock_data(np.array(stars))
+        g.Nobjs, g.d = K, 3 * K
+        q_true = stars_to_q(g, stars)
+        qs, ps = [], []
+        for t in range(4):
+            q = q_true.copy()
+            q[0::3] *= np.exp(0.2 * rs.randn(K))
+            q[1::3] += 0.5 * rs.randn(K)
+            q[2::3] += 0.5 * rs.randn(K)
+            qs.append(q)
+            ps.append(rs.randn(3 * K) * np.sqrt(np.abs(g.H(q))))
+        qs, ps = np.array(qs), np.array(ps)
+        res = dict(D=g.D, q=qs, p=ps)
+        res["dVdq"] = np.array([g.dVdq(q) for q in qs])
+        res["H"] = np.array([g.H(q) for q in qs])
+        res["dphidq"] = np.array([g.dphidq(q) for q in qs])
+        res["V"] = np.array([g.V(q, f_pos=False) for q in qs])
+        res["Vpos"] = np.array([g.V(q, f_pos=True) for q in qs])
+        res["T"] = np.array([g.T(p, g.H(q)) for q, p in zip(qs, ps)])
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+        print("bigk", name, "done")
+    cases = {"bigk": out}
+    big = dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True)
+    cases["traj_bigk"] = traj_case(
+        S, U, 32, lambda g: powlaw_stars(U, g, 100, 32),
+        lambda g, c: powlaw_stars(U, g, 100, 32), big, 2, 50)
+    cases["traj_bigk256"] = traj_case(
+        S, U, 256, lambda g: powlaw_stars(U, g, 128, 256),
+        lambda g, c: powlaw_stars(U, g, 128, 256), big, 1, 4)
     return cases
 
 
@@ -593,6 +663,12 @@ def main():
             for name, d in case_trajs(S, U).items():
                 np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
                 print("wrote", name)
+        # subsets of the above, regenerated on their own (--only c5 / bigk)
+        for job, fn in (("c5", case_c5), ("bigk", case_bigk)):
+            if args.only == job or (not args.only and job == "bigk"):
+                for name, d in fn(S, U).items():
+                    np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+                    print("wrote", name)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -130,7 +130,7 @@ static void gpu_checks() {
     std::vector<double> reals(3 * 32 * 32);
     CHECK(rhmc_gen_image(ctx, &P, truth, 1, 32, 32, 3, 5, reals.data(), 0) == RHMC_OK, "reals");
 
-    for (int K : {1, 3, 12}) {
+    for (int K : {1, 3, 12, 100}) {
       const int64_t n = (K == 1) ? 37 : 13;  // ragged: not a multiple of any wave size
       std::vector<double> q, p;
       chains(r, n, K, 48, q, p);
@@ -207,8 +207,8 @@ static void gpu_checks() {
         for (int i = 0; i < 6; ++i) fin = fin && std::isfinite(q[c * 6 + i]) && std::isfinite(p[c * 6 + i]);
         CHECK(fin == !(st[c] & RHMC_STATUS_NONFINITE), "NONFINITE flag 32 px chain %d", c);
       }
-      CHECK(rhmc_leapfrog(ctx, &P, q.data(), p.data(), 9, 65, 1, nullptr, nullptr) ==
-                RHMC_ERR_ARG, "K = 65 rejected");
+      CHECK(rhmc_leapfrog(ctx, &P, q.data(), p.data(), 9, 257, 1, nullptr, nullptr) ==
+                RHMC_ERR_ARG, "K = 257 rejected");
       rhmc_params bad = P;
       bad.reserved = 1;
       CHECK(rhmc_leapfrog(ctx, &bad, q.data(), p.data(), 9, 2, 1, nullptr, nullptr) ==

@@ -1,7 +1,8 @@
 """Host AddressSanitizer runs of the C-ABI: the library's host code (argument
 checks, host<->device staging, context lifetime, error strings) built with
 -Xarch_host -fsanitize=address and driven by tests/native/capi_asan.cpp
-(`make -C hmc-stellar-toy-model_amd asan`, also run by __graft_entry__.build()).
+(`make -C hmc-stellar-toy-model_amd asan`: built by the CPU test below when its
+sources changed, and best effort by __graft_entry__.build()).
 Device code is the product's, unsanitised (GPU ASan is not available here).
 ASan aborts the driver on the first heap error, so exit status 0 means every
 check passed with a clean report."""
@@ -23,9 +24,10 @@ def _run(mode, leaks):
 
 def test_capi_error_paths_under_asan():
     """No GPU needed: NULL / bad arguments and the no-device path, leak check on."""
-    if not os.path.exists(BIN):
-        if not os.path.exists("/opt/rocm/bin/hipcc"):
+    if not os.path.exists("/opt/rocm/bin/hipcc"):
+        if not os.path.exists(BIN):
             pytest.skip("hipcc not available to build the ASan driver")
+    else:       # (re)build when the sources changed; a no-op otherwise
         subprocess.run(["make", "-C", PKG_DIR, "-j8", "asan"], check=True, capture_output=True)
     r = _run("cpu", leaks=True)
     assert r.returncode == 0, r.stdout + r.stderr
@@ -35,7 +37,7 @@ def test_capi_error_paths_under_asan():
 
 @pytest.mark.gpu
 def test_capi_every_entry_point_under_asan(gpu_lib):
-    """Every entry point on small ragged batches (K = 1 / 3 / 12, all solvers,
+    """Every entry point on small ragged batches (K = 1 / 3 / 12 / 100, all solvers,
     MH with host and device randoms and records, data generation, image
     resize, two context lifetimes) with the host code under ASan.  Leak
     detection is off: the HIP runtime keeps process-lifetime allocations."""

@@ -40,8 +40,10 @@ def test_c5_shard_split_bit_identical(gpu_lib):
     for ws in (2, 4, 0):
         _same(_run(capi, wl.D, wl.params, wl.q0, wl.p0, 12, ws), ref, "C5 1024 chains ws=%d" % ws)
     # ragged: an odd chain count leaves a half-empty last pair and idle groups
+    # (ws = 2 with an odd pair count: a workgroup's last group holds no chain
+    # and mirrors the workgroup's first one)
     for n in (1, 5, 37):
-        for ws in (1, 4):
+        for ws in (1, 2, 4):
             out = _run(capi, wl.D, wl.params, wl.q0[:n], wl.p0[:n], 12, ws)
             _same(out, tuple(r[:n] for r in ref), "C5 %d chains ws=%d" % (n, ws))
 

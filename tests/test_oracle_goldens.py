@@ -136,3 +136,43 @@ def test_hmc_random_exact(name):
     np.testing.assert_array_equal(Ec, z[name + "/E_chain"])
     np.testing.assert_array_equal(dEc, z[name + "/dE_chain"])
     np.testing.assert_array_equal(Ac, z[name + "/A_chain"])
+
+
+@pytest.mark.parametrize("name", ["b100", "b100vc", "b120", "b128"])
+def test_functions_bigk(name):
+    """K > 64 (RHMC-big-sim3/4 geometry): dVdq, dphidq, V, T of the reference."""
+    z = load_golden("bigk")
+    par = R.params_from_npz(z, name + "/par_")
+    m = R.RefModel(z[name + "/D"], par)
+    qs, ps = z[name + "/q"], z[name + "/p"]
+    assert qs.shape[1] // 3 > 64
+    for i, (q, p) in enumerate(zip(qs, ps)):
+        np.testing.assert_allclose(m.dVdq(q), z[name + "/dVdq"][i], rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(m.dphidq(q), z[name + "/dphidq"][i], rtol=1e-13, atol=1e-13)
+        np.testing.assert_allclose(m.H(q), z[name + "/H"][i], rtol=1e-15)
+        np.testing.assert_allclose(m.V(q), z[name + "/V"][i], rtol=1e-14)
+        vp = m.V(q, f_pos=True)
+        assert np.isinf(vp) == np.isinf(z[name + "/Vpos"][i])
+        np.testing.assert_allclose(m.T(p, m.H(q)), z[name + "/T"][i], rtol=1e-14)
+
+
+@pytest.mark.parametrize("name,chains,steps", [("traj_bigk", 2, 50), ("traj_bigk256", 1, 4),
+                                               ("traj_c5", 1, 8)])
+def test_trajectories_many_stars(name, chains, steps):
+    """K = 100 (32x32), K = 128 (256x256) and C5 (K = 64, 256x256): the oracle
+    reproduces the reference's steps and fixed-point iteration counts."""
+    z = load_golden(name)
+    m = R.RefModel(z["D"], R.params_from_npz(z))
+    for c in range(chains):
+        Q, P, NP, NQ = m.trajectory(z["Q"][c, 0], z["P"][c, 0], steps)
+        np.testing.assert_array_equal(NP, z["n_p"][c, :steps])
+        np.testing.assert_array_equal(NQ, z["n_q"][c, :steps])
+        np.testing.assert_allclose(Q, z["Q"][c, :steps + 1], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(P, z["P"][c, :steps + 1], rtol=1e-8, atol=1e-8)
+
+
+def test_c5_golden_reflects():
+    """traj_c5: 4 chains x 50 reference steps, every chain through the flux wall."""
+    z = load_golden("traj_c5")
+    assert z["Q"].shape[:2] == (4, 51)
+    assert (z["Q"][:, 1:, 0::3] < float(z["par_f_lim"])).any(axis=(1, 2)).all()
