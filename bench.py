@@ -141,14 +141,29 @@ def _free_port():
     return port
 
 
-def spawn_ranks(n):
+def _stop(procs, live, grace=10.0):
+    """SIGTERM the live ranks, then SIGKILL whatever is left after `grace` s."""
+    for k in live:
+        procs[k].terminate()
+    end = time.monotonic() + grace
+    for k in live:
+        try:
+            procs[k].wait(timeout=max(0.1, end - time.monotonic()))
+        except subprocess.TimeoutExpired:
+            procs[k].kill()
+            procs[k].wait()
+
+
+def spawn_ranks(n, timeout):
     """Start n rank processes of this script (one per GPU) and wait for them.
 
     Called before anything touches a GPU (no torch import here).  Each child
     gets RANK = LOCAL_RANK = r, WORLD_SIZE = n and a 127.0.0.1 rendezvous;
     rank 0's stdout (the JSON line) is relayed, the other ranks' stdout goes
-    to stderr.  If a rank fails, the others are terminated and the exit code
-    is non-zero."""
+    to stderr.  If a rank fails, the others are stopped and the exit code is
+    non-zero; if the ranks are not all done `timeout` seconds after the start
+    (a rank stuck in the rendezvous, a barrier or a GPU call), every rank is
+    stopped (SIGTERM, SIGKILL 10 s later) and the exit code is 124."""
     port = _free_port()
     procs, outs = [], []
     for r in range(n):
@@ -161,6 +176,7 @@ def spawn_ranks(n):
         outs.append(out)
     rc = 0
     live = set(range(n))
+    deadline = time.monotonic() + timeout
     while live:
         for r in sorted(live):
             code = procs[r].poll()
@@ -171,8 +187,14 @@ def spawn_ranks(n):
                 rc = code if code > 0 else 1
                 sys.stderr.write("bench.py: rank %d exited with %d; stopping the others\n"
                                  % (r, code))
-                for k in live:
-                    procs[k].terminate()
+                _stop(procs, live)
+                live.clear()
+        if live and time.monotonic() > deadline:
+            sys.stderr.write("bench.py: ranks %s still running after --timeout %g s; "
+                             "stopping every rank\n" % (sorted(live), timeout))
+            _stop(procs, live)
+            live.clear()
+            rc = 124
         time.sleep(0.05)
     for r, out in enumerate(outs):
         out.seek(0)
@@ -183,16 +205,40 @@ def spawn_ranks(n):
     return rc
 
 
-def load_pmc(workload):
+# Sources whose bytes decide the kernels' machine code: the PMC summaries
+# record their hash, and a summary taken on other sources is not used.
+SOURCE_GLOBS = ("hmc-stellar-toy-model_amd/csrc/*", "hmc-stellar-toy-model_amd/Makefile",
+                "include/rhmc.h")
+
+
+def source_hash(root=ROOT):
+    """sha256 (16 hex digits) over the kernel sources, path + bytes, in path order."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted({f for g in SOURCE_GLOBS for f in glob.glob(os.path.join(root, g))
+                    if os.path.isfile(f)})
+    for f in files:
+        h.update(os.path.relpath(f, root).replace(os.sep, "/").encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def load_pmc(workload, root=ROOT):
     """rocprofv3 PMC summary of the dominant kernel (profiles/pmc_<wl>.json,
     written by scripts/pmc_summary.py): HBM bytes per launch and executed
-    fp64 flops per chain-step."""
-    path = os.path.join(ROOT, "profiles", "pmc_%s.json" % workload.lower())
+    fp64 flops per chain-step.  Returns (summary, stale): a summary whose
+    `src_hash` is missing or differs from the shipped sources' is stale — its
+    counters describe other machine code, so roofline() reports no fraction."""
+    path = os.path.join(root, "profiles", "pmc_%s.json" % workload.lower())
     try:
         with open(path) as fh:
-            return json.load(fh)
+            pmc = json.load(fh)
     except (OSError, ValueError):
-        return {}
+        return {}, False
+    return pmc, pmc.get("src_hash") != source_hash(root)
 
 
 def bench_datagen(args, wl, P, ctx, dev, stream, world, rank):
@@ -284,6 +330,10 @@ def main():
     ap.add_argument("--n-real", type=int, default=1000)
     ap.add_argument("--dry-run", action="store_true",
                     help="rendezvous the ranks and print the sharding plan; no GPU work")
+    ap.add_argument("--timeout", type=float, default=900.0,
+                    help="seconds: --gpus N (spawned ranks) stops every rank and exits 124 "
+                         "when they are not all done by then; each rank's gloo rendezvous "
+                         "and barriers time out after it too")
     args = ap.parse_args()
 
     env_world = os.environ.get("WORLD_SIZE")
@@ -293,7 +343,7 @@ def main():
             raise SystemExit("bench.py: --gpus must be >= 1")
         if n > 1:
             # one process per GPU: start the ranks before any GPU call here
-            return spawn_ranks(n)
+            return spawn_ranks(n, args.timeout)
         world = 1
     else:
         world = int(env_world)
@@ -302,6 +352,7 @@ def main():
                              % (args.gpus, world))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    _fault_injection(rank)
 
     from rhmc_amd import shard, workloads
     if args.workload.upper() in ("C4", "C5") and not args.chains and not args.global_chains:
@@ -331,7 +382,7 @@ def main():
     from rhmc_amd import capi
 
     if world > 1:
-        dist.init_process_group("gloo")
+        init_gloo(args.timeout)
     ndev = torch.cuda.device_count()
     if gpu >= ndev:
         raise SystemExit("bench.py: rank %d wants GPU %d but %d are visible"
@@ -399,10 +450,20 @@ def main():
         b.record(stream)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
+    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    steps_per_launch = leap * (args.mh_iter if args.mode == "mh" else 1)
+    per_rank = None
     if world > 1:
         dist.barrier()
-        wall = shard.max_over_ranks(wall)
-    launch_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+        mine = {"rank": rank, "gpu": gpu, "chains": int(wl.n_chains), "wall_s": wall,
+                "kernel_ms": launch_ms,
+                "value": wl.n_chains * steps_per_launch * args.steps / wall}
+        per_rank = [None] * world
+        dist.all_gather_object(per_rank, mine)
+        wall = max(r["wall_s"] for r in per_rank)          # max over ranks
+        vals = [r["value"] for r in per_rank]
+        per_rank = {"ranks": per_rank, "min": min(vals), "max": max(vals),
+                    "imbalance": max(vals) / min(vals) if min(vals) > 0 else None}
 
     stat = st.cpu().numpy()
     nonfinite = int(((stat & capi.STATUS_NONFINITE) != 0).sum())
@@ -418,11 +479,10 @@ def main():
                 "near_wall_chains": int(((stat & capi.STATUS_NEAR_WALL) != 0).sum()),
                 "near_wall_frac": float(((stat & capi.STATUS_NEAR_WALL) != 0).mean())}
 
-    steps_per_launch = leap * (args.mh_iter if args.mode == "mh" else 1)
     chain_steps = wl.n_chains * steps_per_launch
     value = total_chains * steps_per_launch * args.steps / wall
     # PMC summaries describe the implicit leapfrog kernel only
-    pmc = load_pmc(wl.name) if args.mode == "leapfrog" else {}
+    pmc, stale = load_pmc(wl.name) if args.mode == "leapfrog" else ({}, False)
     metric = "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X"
     if wl.name != "C2" or args.chains or args.global_chains or args.mode != "leapfrog":
         # not the headline configuration: name what was run
@@ -451,9 +511,10 @@ def main():
                    "solver": (args.solver if args.mode == "integrate" else
                               "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},
-        "roofline": roofline(pmc, wl, chain_steps, launch_ms),
+        "roofline": roofline(pmc, wl, chain_steps, launch_ms, stale),
         "nonfinite_chains": nonfinite,
         "fixed_point_iters_per_step": fp_stats,
+        "per_rank": per_rank,
     }
     if args.mode == "leapfrog" and not args.no_e2e and world == 1:
         out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)
@@ -465,7 +526,7 @@ def main():
         dist.destroy_process_group()
 
 
-def roofline(pmc, wl, chain_steps, launch_ms):
+def roofline(pmc, wl, chain_steps, launch_ms, stale=False):
     """The roof that binds the dominant kernel: fp64 VALU issue.
 
     The image is LDS-resident and each chain's window pixels sit in VGPRs, so
@@ -477,8 +538,14 @@ def roofline(pmc, wl, chain_steps, launch_ms):
     (2*FETCH_SIZE + WRITE_SIZE, gfx950 correction), `hbm_measured_frac` its
     rate over 8 TB/s.  `alg_model` keeps SURVEY §8(d)'s algorithmic-bytes model
     (D read by both gradients + q/p in/out per chain-step), which exceeds the
-    HBM peak by construction because D never leaves the chip."""
+    HBM peak by construction because D never leaves the chip.
+    stale: the summary was taken on other kernel sources (load_pmc) — its
+    counters are not used (achieved / frac / traffic null, pmc_stale true)."""
     s = launch_ms * 1e-3
+    if stale:
+        pmc = dict(pmc, hbm_bytes_per_launch=None, fp64_flops_per_chain_step=None,
+                   valu_active_frac=None, simd_valu_issue_frac=None,
+                   valu_insts_per_chain_step=None)
     traffic = pmc.get("hbm_bytes_per_launch")
     per = pmc.get("chain_steps_per_dispatch")
     if traffic is not None and per not in (None, chain_steps):
@@ -499,9 +566,11 @@ def roofline(pmc, wl, chain_steps, launch_ms):
         "valu_active_frac": pmc.get("valu_active_frac"),
         "simd_valu_issue_frac": pmc.get("simd_valu_issue_frac"),
         "valu_insts_per_chain_step": pmc.get("valu_insts_per_chain_step"),
-        "pmc_source": ("profiles/pmc_%s.json (%s, revision %s)"
-                       % (wl.name.lower(), pmc.get("kernel", "?"), pmc.get("head", "?"))
+        "pmc_source": ("profiles/pmc_%s.json (%s, revision %s, sources %s)"
+                       % (wl.name.lower(), pmc.get("kernel", "?"), pmc.get("head", "?"),
+                          pmc.get("src_hash", "?"))
                        if pmc else None),
+        "pmc_stale": bool(stale),
         "hbm_measured_gbs": None if traffic is None else traffic / s / 1e9,
         "hbm_measured_frac": None if traffic is None else traffic / s / 1e9 / HBM_PEAK_GBS,
         "alg_model": {
@@ -514,6 +583,25 @@ def roofline(pmc, wl, chain_steps, launch_ms):
     }
 
 
+def init_gloo(timeout):
+    """The ranks' host-side process group (barriers, timing max, per-rank
+    rates): gloo over 127.0.0.1, every collective bounded by `timeout` + 30 s
+    (the launcher's own deadline, counted from the spawn, fires first)."""
+    import datetime
+    import torch.distributed as dist
+    dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout + 30.0))
+
+
+def _fault_injection(rank):
+    """RHMC_BENCH_FAULT_SLEEP=<rank>:<seconds> makes that rank sleep before
+    its rendezvous (tests/test_bench_launch.py: the launcher's --timeout)."""
+    spec = os.environ.get("RHMC_BENCH_FAULT_SLEEP")
+    if spec:
+        r, secs = spec.split(":")
+        if int(r) == rank:
+            time.sleep(float(secs))
+
+
 def dry_run(args, wl, world, rank, gpu, total_chains):
     """The sharding plan every rank would run, gathered over gloo: no GPU
     work.  Rank 0 prints one JSON line."""
@@ -522,7 +610,7 @@ def dry_run(args, wl, world, rank, gpu, total_chains):
     plans = [plan]
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("gloo")
+        init_gloo(args.timeout)
         plans = [None] * world
         dist.all_gather_object(plans, plan)
         dist.barrier()

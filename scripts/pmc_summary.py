@@ -14,6 +14,9 @@ import os
 import sys
 from collections import defaultdict
 
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from bench import source_hash  # noqa: E402  (the hash bench.py checks)
+
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_c2"
 wl = sys.argv[2] if len(sys.argv) > 2 else "c2"
 kernel_sub = sys.argv[3] if len(sys.argv) > 3 else "leapfrog"
@@ -32,7 +35,7 @@ for path in glob.glob(os.path.join(root, "*", "**", "*counter_collection.csv"), 
 
 avg = {k: sum(v) / len(v) for k, v in vals.items() if v}
 out = {"workload": wl, "kernel_filter": kernel_sub, "kernel": " | ".join(sorted(names)),
-       "head": head, "counters_avg_per_dispatch": avg}
+       "head": head, "src_hash": source_hash(), "counters_avg_per_dispatch": avg}
 if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
     out["hbm_bytes_per_launch"] = (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024
 f64 = ("SQ_INSTS_VALU_FMA_F64", "SQ_INSTS_VALU_MUL_F64", "SQ_INSTS_VALU_ADD_F64")

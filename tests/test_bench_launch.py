@@ -29,7 +29,7 @@ def _line(out):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("n", [1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 8])
 def test_gpus_flag_reaches_the_rank_count(n):
     out = _bench(["--gpus", str(n), "--dry-run"])
     assert out.returncode == 0, out.stderr[-3000:]
@@ -54,15 +54,17 @@ def test_gpus_flag_with_pinned_device():
     assert d["n_gpus"] == 2 and {r["gpu"] for r in d["ranks"]} == {0}
 
 
-@pytest.mark.parametrize("wl,total", [("C4", 1 << 20), ("C5", 8192)])
-def test_global_set_is_split_not_replicated(wl, total):
+@pytest.mark.parametrize("wl,total,n", [("C4", 1 << 20, 2), ("C5", 8192, 2), ("C5", 8192, 8)])
+def test_global_set_is_split_not_replicated(wl, total, n):
     """C4 = one 2^20-chain set, C5 one 8192-chain set, split over the ranks
     (strong scaling, BASELINE configs[3], [4])."""
-    out = _bench(["--gpus", "2", "--dry-run", "--workload", wl])
+    out = _bench(["--gpus", str(n), "--dry-run", "--workload", wl])
     assert out.returncode == 0, out.stderr[-3000:]
     d = _line(out)
+    assert d["n_gpus"] == n
     assert d["config"]["total_chains"] == total
     assert sum(r["chains"] for r in d["ranks"]) == total
+    assert sorted(r["gpu"] for r in d["ranks"]) == list(range(n))
     assert d["scaling"] == "strong"
 
 
@@ -78,3 +80,16 @@ def test_failing_rank_fails_the_launch():
     """A rank that dies makes the launcher exit non-zero (and stop the rest)."""
     out = _bench(["--gpus", "2", "--dry-run", "--workload", "nope"])
     assert out.returncode != 0
+
+
+def test_stuck_rank_hits_the_timeout():
+    """A rank that never reaches the rendezvous: the launcher stops every rank
+    at --timeout and exits 124 instead of waiting for the driver's kill."""
+    import time
+    t = time.monotonic()
+    out = _bench(["--gpus", "2", "--dry-run", "--timeout", "20"],
+                 {"RHMC_BENCH_FAULT_SLEEP": "1:600"})
+    took = time.monotonic() - t
+    assert out.returncode == 124, (out.returncode, out.stderr[-2000:])
+    assert "still running after --timeout" in out.stderr
+    assert took < 60, took

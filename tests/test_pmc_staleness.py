@@ -1,0 +1,65 @@
+"""bench.py's roofline uses a PMC summary only when it was taken on the
+shipped kernel sources: scripts/pmc_summary.py records source_hash() (csrc/*,
+the Makefile, include/rhmc.h) and load_pmc() marks a summary with another or
+no hash stale, which nulls roofline.frac (every roofline must be
+reproducible)."""
+import json
+import os
+import shutil
+
+import bench
+
+ROOT = bench.ROOT
+
+
+class _WL:
+    name = "C2"
+    K = 1
+
+    class D:
+        size = 48 * 48
+
+
+def _tree(tmp_path):
+    for g in ("hmc-stellar-toy-model_amd/csrc", "include"):
+        shutil.copytree(os.path.join(ROOT, g), os.path.join(tmp_path, g))
+    shutil.copy(os.path.join(ROOT, "hmc-stellar-toy-model_amd", "Makefile"),
+                os.path.join(tmp_path, "hmc-stellar-toy-model_amd", "Makefile"))
+    os.makedirs(os.path.join(tmp_path, "profiles"))
+    pmc = {"fp64_flops_per_chain_step": 12000.0, "hbm_bytes_per_launch": 7e5,
+           "chain_steps_per_dispatch": 2048000.0, "kernel": "k", "head": "h",
+           "src_hash": bench.source_hash(str(tmp_path))}
+    with open(os.path.join(tmp_path, "profiles", "pmc_c2.json"), "w") as fh:
+        json.dump(pmc, fh)
+    return str(tmp_path)
+
+
+def test_fresh_summary_gives_a_fraction(tmp_path):
+    root = _tree(tmp_path)
+    pmc, stale = bench.load_pmc("C2", root)
+    assert not stale
+    r = bench.roofline(pmc, _WL, 2048000, 1.0, stale)
+    assert r["frac"] is not None and not r["pmc_stale"]
+    assert abs(r["achieved"] - 12000.0 * 2048000 / 1e-3 / 1e12) < 1e-9
+
+
+def test_one_flipped_byte_makes_it_stale(tmp_path):
+    root = _tree(tmp_path)
+    src = os.path.join(root, "hmc-stellar-toy-model_amd", "csrc", "rhmc_tiledr.hpp")
+    b = bytearray(open(src, "rb").read())
+    b[len(b) // 2] ^= 1
+    open(src, "wb").write(bytes(b))
+    pmc, stale = bench.load_pmc("C2", root)
+    assert stale
+    r = bench.roofline(pmc, _WL, 2048000, 1.0, stale)
+    assert r["frac"] is None and r["achieved"] is None and r["traffic"] is None
+    assert r["pmc_stale"] is True
+
+
+def test_summary_without_hash_is_stale(tmp_path):
+    root = _tree(tmp_path)
+    path = os.path.join(root, "profiles", "pmc_c2.json")
+    pmc = json.load(open(path))
+    del pmc["src_hash"]
+    json.dump(pmc, open(path, "w"))
+    assert bench.load_pmc("C2", root)[1]
