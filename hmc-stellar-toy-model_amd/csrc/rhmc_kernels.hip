@@ -1629,10 +1629,28 @@ bool mh_pk_fused(const rhmc_ctx* ctx, const Consts& c, int K) {
   return use_pixk(ctx, K, c);
 }
 
+// The run's parameters at MH iteration l: multi_gym.run_RHMC's schedules
+// (sampler_RHMC.py:1010-1016) set g_ff2 = schedule_g_ff2[l] and beta =
+// schedule_beta[l] while l < the schedule's size and keep the last value
+// after it; no schedule keeps P's value.
+rhmc_params sched_params(const rhmc_params& P, const rhmc_mh_schedule* sc, int l) {
+  rhmc_params q = P;
+  if (sc && sc->g_ff2 && sc->n_g_ff2 > 0) q.g_ff2 = sc->g_ff2[l < sc->n_g_ff2 ? l : sc->n_g_ff2 - 1];
+  if (sc && sc->beta && sc->n_beta > 0) q.beta = sc->beta[l < sc->n_beta ? l : sc->n_beta - 1];
+  return q;
+}
+
+bool sched_active(const rhmc_mh_schedule* sc) {
+  return sc && ((sc->g_ff2 && sc->n_g_ff2 > 0) || (sc->beta && sc->n_beta > 0));
+}
+
 // V(q) once, then one mh_pk_iter launch per iteration (rhmc_mhpk.hpp); V
-// [n] is the carried V(q) (device scratch).
+// [n] is the carried V(q) (device scratch).  A schedule changes only g_ff2
+// and beta, which this kernel's V does not read (no repulsion here), so the
+// carried V stays exact; each launch gets its iteration's constants.
 template <int IMG>
-int launch_mh_pk(const rhmc_ctx* ctx, MhKArgs k, double* V, hipStream_t s) {
+int launch_mh_pk(const rhmc_ctx* ctx, MhKArgs k, double* V, hipStream_t s,
+                 const rhmc_params* P, const rhmc_mh_schedule* sc) {
   using MP = MhPK<IMG, 10>;
   int W = 4;
   while (W > 1 && MP::lds_bytes(W) > (size_t)ctx->max_lds / 2) W >>= 1;
@@ -1644,6 +1662,11 @@ int launch_mh_pk(const rhmc_ctx* ctx, MhKArgs k, double* V, hipStream_t s) {
   hipLaunchKernelGGL((mh_pk_v0<IMG, 10>), grid, block, lds, s, k, V);
   HIP_TRY(hipGetLastError());
   for (int it = 0; it < k.n_iter; ++it) {
+    if (sched_active(sc)) {
+      const rhmc_params Pl = sched_params(*P, sc, it);
+      int rc = make_consts(&Pl, &k.c);
+      if (rc) return rc;
+    }
     hipLaunchKernelGGL((mh_pk_iter<IMG, 10>), grid, block, lds, s, k, it, V);
     HIP_TRY(hipGetLastError());
   }
@@ -1652,14 +1675,27 @@ int launch_mh_pk(const rhmc_ctx* ctx, MhKArgs k, double* V, hipStream_t s) {
 
 // The MH outer loop on device buffers (sampler_RHMC.py:1018-1083): per
 // iteration begin -> n_steps fused leapfrog -> V(q') -> accept, all queued on
-// `s` with no host synchronisation.  `rec` holds device pointers (nullable).
+// `s` with no host synchronisation.  `rec` holds device pointers (nullable);
+// `sc` (nullable, host arrays) schedules g_ff2 / beta per iteration
+// (sampler_RHMC.py:1010-1016, sched_params).
 int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t K,
            int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z, const double* d_u,
-           uint64_t seed, const rhmc_mh_record* rec, hipStream_t s) {
+           uint64_t seed, const rhmc_mh_record* rec, hipStream_t s,
+           const rhmc_mh_schedule* sc = nullptr) {
   Consts c;
   int rc = make_consts(P, &c);
   if (rc) return rc;
   if (n_iter < 0 || n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter/n_steps < 0");
+  if (sc && (sc->n_g_ff2 < 0 || sc->n_beta < 0 || (sc->n_g_ff2 > 0 && !sc->g_ff2) ||
+             (sc->n_beta > 0 && !sc->beta)))
+    return fail(RHMC_ERR_ARG, "schedule: negative size or NULL array with a nonzero size");
+  const bool sched = sched_active(sc);
+  if (sched)  // every iteration's parameters must be valid, not only the first's
+    for (int it = 0; it < n_iter; ++it) {
+      const rhmc_params Pl = sched_params(*P, sc, it);
+      Consts cl;
+      if ((rc = make_consts(&Pl, &cl))) return rc;
+    }
   if (n == 0 || n_iter == 0) return RHMC_OK;
   if (K == 1 && mh_k1_fused(ctx, c, n)) {
     MhK1Args k;
@@ -1677,14 +1713,27 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
     k.n_iter = n_iter;
     k.n_steps = n_steps;
     k.f_pos = f_pos != 0 ? RHMC_V_FLUX_WALL : 0;
-    k.pad = 0;
+    k.it0 = 0;
     k.seed = seed;
     k.c = c;
-    switch (ctx->rows) {
-      case 32: return launch_mh_k1<32>(ctx, k, s);
-      case 48: return launch_mh_k1<48>(ctx, k, s);
-      default: return launch_mh_k1<64>(ctx, k, s);
+    auto launch = [&]() {
+      switch (ctx->rows) {
+        case 32: return launch_mh_k1<32>(ctx, k, s);
+        case 48: return launch_mh_k1<48>(ctx, k, s);
+        default: return launch_mh_k1<64>(ctx, k, s);
+      }
+    };
+    if (!sched) return launch();
+    // scheduled: one launch per iteration with its own constants (V(q) is
+    // re-evaluated at each launch's start: the same operations, the same value)
+    for (int it = 0; it < n_iter; ++it) {
+      const rhmc_params Pl = sched_params(*P, sc, it);
+      if ((rc = make_consts(&Pl, &k.c))) return rc;
+      k.n_iter = 1;
+      k.it0 = it;
+      if ((rc = launch())) return rc;
     }
+    return RHMC_OK;
   }
   if (K >= 2 && mh_pk_fused(ctx, c, K)) {
     MhKArgs k;
@@ -1714,7 +1763,8 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
       ctx->mh_scratch_bytes = need;
     }
     double* V = (double*)ctx->mh_scratch;
-    return ctx->rows == 32 ? launch_mh_pk<32>(ctx, k, V, s) : launch_mh_pk<48>(ctx, k, V, s);
+    return ctx->rows == 32 ? launch_mh_pk<32>(ctx, k, V, s, P, sc)
+                           : launch_mh_pk<48>(ctx, k, V, s, P, sc);
   }
   const size_t sb = (size_t)n * 3 * K * sizeof(double), eb = (size_t)n * sizeof(double);
   const size_t need = 2 * sb + 3 * eb + 256;
@@ -1747,14 +1797,24 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   m.c = c;
   f_pos = f_pos != 0 ? RHMC_V_FLUX_WALL : 0;
   if ((rc = launch_energy(ctx, c, d_q, nullptr, m.V_cur, nullptr, n, K, f_pos, s))) return rc;
+  // V reads beta through the repulsion term: a beta schedule re-evaluates
+  // V(q) at each iteration's start, like the reference's V_initial (:1025)
+  const bool v_sched = sched && c.use_Vc && sc->beta && sc->n_beta > 0;
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
   for (int it = 0; it < n_iter; ++it) {
     m.iter = it;
+    const rhmc_params Pl = sched ? sched_params(*P, sc, it) : *P;
+    if (sched) {
+      if ((rc = make_consts(&Pl, &m.c))) return rc;
+      if (v_sched &&
+          (rc = launch_energy(ctx, m.c, d_q, nullptr, m.V_cur, nullptr, n, K, f_pos, s)))
+        return rc;
+    }
     hipLaunchKernelGGL(mh_begin_kernel, grid, block, 0, s, m);
     HIP_TRY(hipGetLastError());
-    if ((rc = launch_leapfrog(ctx, P, m.q_prop, m.p, n, K, n_steps, nullptr, nullptr, s)))
+    if ((rc = launch_leapfrog(ctx, &Pl, m.q_prop, m.p, n, K, n_steps, nullptr, nullptr, s)))
       return rc;
-    if ((rc = launch_energy(ctx, c, m.q_prop, nullptr, m.V_prop, nullptr, n, K, f_pos, s)))
+    if ((rc = launch_energy(ctx, m.c, m.q_prop, nullptr, m.V_prop, nullptr, n, K, f_pos, s)))
       return rc;
     hipLaunchKernelGGL(mh_end_kernel, grid, block, 0, s, m);
     HIP_TRY(hipGetLastError());
@@ -2301,20 +2361,37 @@ int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const doub
   return RHMC_OK;
 }
 
-int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
-                   int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
-                   const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream) {
+int rhmc_mh_scheduled_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
+                             int64_t n_chains, int32_t K, int32_t n_iter, int32_t n_steps,
+                             int32_t f_pos, const double* d_z, const double* d_u, uint64_t seed,
+                             const rhmc_mh_record* rec, const rhmc_mh_schedule* sched,
+                             void* stream) {
   int rc = check_common(ctx, n_chains, K);
   if (rc) return rc;
   if (n_chains > 0 && !d_q) return fail(RHMC_ERR_ARG, "q is NULL");
   HIP_TRY(hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  return run_mh(ctx, P, d_q, n_chains, K, n_iter, n_steps, f_pos, d_z, d_u, seed, rec, s);
+  return run_mh(ctx, P, d_q, n_chains, K, n_iter, n_steps, f_pos, d_z, d_u, seed, rec, s, sched);
+}
+
+int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
+                   int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
+                   const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream) {
+  return rhmc_mh_scheduled_device(ctx, P, d_q, n_chains, K, n_iter, n_steps, f_pos, d_z, d_u,
+                                  seed, rec, nullptr, stream);
 }
 
 int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, int32_t K,
             int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* z, const double* u,
             uint64_t seed, const rhmc_mh_record* rec) {
+  return rhmc_mh_scheduled(ctx, P, q, n_chains, K, n_iter, n_steps, f_pos, z, u, seed, rec,
+                           nullptr);
+}
+
+int rhmc_mh_scheduled(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains,
+                      int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* z,
+                      const double* u, uint64_t seed, const rhmc_mh_record* rec,
+                      const rhmc_mh_schedule* sched) {
   int rc = check_common(ctx, n_chains, K);
   if (rc) return rc;
   if (n_chains == 0 || n_iter == 0) return RHMC_OK;
@@ -2350,7 +2427,7 @@ int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, in
   if (z) HIP_TRY(hipMemcpyAsync((void*)dz, z, zb, hipMemcpyHostToDevice, ctx->stream));
   if (u) HIP_TRY(hipMemcpyAsync((void*)du, u, ub, hipMemcpyHostToDevice, ctx->stream));
   if ((rc = run_mh(ctx, P, dq, n_chains, K, n_iter, n_steps, f_pos, dz, du, seed, &drec,
-                   ctx->stream)))
+                   ctx->stream, sched)))
     return rc;
   HIP_TRY(hipMemcpyAsync(q, dq, sb, hipMemcpyDeviceToHost, ctx->stream));
   if (rec) {

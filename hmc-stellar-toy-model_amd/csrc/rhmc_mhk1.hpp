@@ -33,7 +33,8 @@ struct MhK1Args {
   double* T_chain;        // nullable [n_iter][n]
   int32_t* accept;        // nullable [n_iter][n]
   int64_t n;
-  int n_iter, n_steps, f_pos, pad;
+  int n_iter, n_steps, f_pos;
+  int it0;                // index of the launch's first iteration (RNG keys, record rows)
   unsigned long long seed;
   Consts c;
 };
@@ -121,11 +122,12 @@ mh_k1_tiledr(MhK1Args a) {
     if (it < 0) {
       V0 = V1;
     } else {
-      const int64_t r = (int64_t)it * a.n + chr;
+      const int gi = a.it0 + it;                   // the run's iteration index
+      const int64_t r = (int64_t)gi * a.n + chr;
       const double q3p[3] = {f1, x1, y1};
       const double p3p[3] = {pf, px, py};
       const double dE = (V1 + kinetic(q3p, p3p, 1, c)) - E0;
-      const double uu = a.u ? a.u[r] : philox_uniform(a.seed, chr, it);
+      const double uu = a.u ? a.u[r] : philox_uniform(a.seed, chr, gi);
       const bool acc = (dE < 0.0) || (log(uu) < -dE);  // :1076
       if (acc) {
         f = f1;
@@ -137,7 +139,8 @@ mh_k1_tiledr(MhK1Args a) {
     }
     const int nx = it + 1;
     if (nx == a.n_iter) break;
-    const int64_t r = (int64_t)nx * a.n + chr;
+    const int gn = a.it0 + nx;                     // the run's iteration index
+    const int64_t r = (int64_t)gn * a.n + chr;
     double hff, hxx;
     metric_pair(f, c, hff, hxx);
     double z0, z1, z2;
@@ -146,9 +149,9 @@ mh_k1_tiledr(MhK1Args a) {
       z1 = a.z[3 * r + 1];
       z2 = a.z[3 * r + 2];
     } else {
-      z0 = philox_normal(a.seed, chr, nx, 0);
-      z1 = philox_normal(a.seed, chr, nx, 1);
-      z2 = philox_normal(a.seed, chr, nx, 2);
+      z0 = philox_normal(a.seed, chr, gn, 0);
+      z1 = philox_normal(a.seed, chr, gn, 1);
+      z2 = philox_normal(a.seed, chr, gn, 2);
     }
     pf = z0 * sqrt(hff);                           // :1022
     px = z1 * sqrt(hxx);

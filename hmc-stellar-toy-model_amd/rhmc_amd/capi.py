@@ -48,7 +48,8 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
            "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
            "rhmc_gen_image", "rhmc_gen_image_device", "rhmc_hmc_random",
-           "rhmc_hmc_random_device")
+           "rhmc_hmc_random_device", "rhmc_mh_scheduled", "rhmc_mh_scheduled_device")
+ABI_VERSION = 3
 
 V_FLUX_WALL = 1       # rhmc_energy f_pos bits (include/rhmc.h)
 V_NO_POSCHECK = 2
@@ -80,6 +81,25 @@ class MhRecord(ctypes.Structure):
     _fields_ = [("q_chain", ctypes.c_void_p), ("E_chain", ctypes.c_void_p),
                 ("V_chain", ctypes.c_void_p), ("T_chain", ctypes.c_void_p),
                 ("accept", ctypes.c_void_p)]
+
+
+class MhSchedule(ctypes.Structure):
+    """Mirror of `rhmc_mh_schedule` (include/rhmc.h): host arrays."""
+    _fields_ = [("g_ff2", ctypes.c_void_p), ("beta", ctypes.c_void_p),
+                ("n_g_ff2", ctypes.c_int32), ("n_beta", ctypes.c_int32)]
+
+
+def make_schedule(schedule_g_ff2=None, schedule_beta=None):
+    """(MhSchedule, arrays to keep alive) for run_RHMC's schedule_g_ff2 /
+    schedule_beta (sampler_RHMC.py:1010-1016), or (None, ()) without one."""
+    if schedule_g_ff2 is None and schedule_beta is None:
+        return None, ()
+    g = None if schedule_g_ff2 is None else _f64(np.ravel(schedule_g_ff2), "schedule_g_ff2")
+    b = None if schedule_beta is None else _f64(np.ravel(schedule_beta), "schedule_beta")
+    sc = MhSchedule(None if g is None or g.size == 0 else g.ctypes.data,
+                    None if b is None or b.size == 0 else b.ctypes.data,
+                    0 if g is None else g.size, 0 if b is None else b.size)
+    return sc, (g, b)
 
 
 class RhmcError(RuntimeError):
@@ -131,6 +151,15 @@ def _load():
         "rhmc_mh_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64, ctypes.c_int32,
                                           ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, vp, vp,
                                           ctypes.c_uint64, P(MhRecord), vp]),
+        "rhmc_mh_scheduled": (ctypes.c_int, [vp, P(RhmcParams), c_dp, ctypes.c_int64,
+                                             ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                             ctypes.c_int32, c_dp, c_dp, ctypes.c_uint64,
+                                             P(MhRecord), P(MhSchedule)]),
+        "rhmc_mh_scheduled_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64,
+                                                    ctypes.c_int32, ctypes.c_int32,
+                                                    ctypes.c_int32, ctypes.c_int32, vp, vp,
+                                                    ctypes.c_uint64, P(MhRecord), P(MhSchedule),
+                                                    vp]),
         "rhmc_hmc_random": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_ip,
                                            ctypes.c_int64, ctypes.c_int32, c_ip]),
         "rhmc_hmc_random_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, vp, vp,
@@ -330,12 +359,15 @@ class Context:
             return V[0], (None if T is None else T[0])
         return V, T
 
-    def mh(self, params, q, n_iter, n_steps, f_pos=True, z=None, u=None, seed=0, record=True):
+    def mh(self, params, q, n_iter, n_steps, f_pos=True, z=None, u=None, seed=0, record=True,
+           schedule_g_ff2=None, schedule_beta=None):
         """n_iter MH iterations (run_RHMC move-0 branch) of n_steps leapfrog steps
         on every chain of q [n_chains, 3K].  z [n_iter, n_chains, 3K] / u
-        [n_iter, n_chains]: host randoms (None = Philox on device).  Returns a
-        dict with the final q and, when record, q_chain/E_chain/V_chain/T_chain
-        [n_iter, n_chains(, 3K)] and accept [n_iter, n_chains]."""
+        [n_iter, n_chains]: host randoms (None = Philox on device).
+        schedule_g_ff2 / schedule_beta: run_RHMC's per-iteration schedules
+        (rhmc_mh_scheduled).  Returns a dict with the final q and, when record,
+        q_chain/E_chain/V_chain/T_chain [n_iter, n_chains(, 3K)] and accept
+        [n_iter, n_chains]."""
         q2 = np.array(q, dtype=np.float64, order="C", copy=True)
         single = q2.ndim == 1
         q2 = q2.reshape(1, -1) if single else q2.reshape(-1, q2.shape[-1])
@@ -352,23 +384,29 @@ class Context:
             rec = MhRecord(out["q_chain"].ctypes.data, out["E_chain"].ctypes.data,
                            out["V_chain"].ctypes.data, out["T_chain"].ctypes.data,
                            out["accept"].ctypes.data)
-        _check(_lib.rhmc_mh(self._h, ctypes.byref(params), _dptr(q2), n, d // 3, int(n_iter),
-                            int(n_steps), int(bool(f_pos)),
-                            None if zz is None else _dptr(zz), None if uu is None else _dptr(uu),
-                            ctypes.c_uint64(int(seed)), None if rec is None else ctypes.byref(rec)))
+        sc, keep = make_schedule(schedule_g_ff2, schedule_beta)
+        _check(_lib.rhmc_mh_scheduled(
+            self._h, ctypes.byref(params), _dptr(q2), n, d // 3, int(n_iter), int(n_steps),
+            int(bool(f_pos)), None if zz is None else _dptr(zz),
+            None if uu is None else _dptr(uu), ctypes.c_uint64(int(seed)),
+            None if rec is None else ctypes.byref(rec), None if sc is None else ctypes.byref(sc)))
+        del keep
         out["q"] = q2[0] if single else q2
         return out
 
     def mh_device(self, params, q_ptr, n_chains, K, n_iter, n_steps, f_pos=True, z_ptr=None,
-                  u_ptr=None, seed=0, record=None, stream=None):
+                  u_ptr=None, seed=0, record=None, stream=None, schedule_g_ff2=None,
+                  schedule_beta=None):
         """Device-pointer variant (asynchronous on `stream`); record: MhRecord of
-        device pointers or None."""
-        _check(_lib.rhmc_mh_device(self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr),
-                                   int(n_chains), int(K), int(n_iter), int(n_steps),
-                                   int(bool(f_pos)), ctypes.c_void_p(z_ptr or 0),
-                                   ctypes.c_void_p(u_ptr or 0), ctypes.c_uint64(int(seed)),
-                                   None if record is None else ctypes.byref(record),
-                                   ctypes.c_void_p(stream or 0)))
+        device pointers or None; schedules: host arrays (read during the call)."""
+        sc, keep = make_schedule(schedule_g_ff2, schedule_beta)
+        _check(_lib.rhmc_mh_scheduled_device(
+            self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr), int(n_chains), int(K),
+            int(n_iter), int(n_steps), int(bool(f_pos)), ctypes.c_void_p(z_ptr or 0),
+            ctypes.c_void_p(u_ptr or 0), ctypes.c_uint64(int(seed)),
+            None if record is None else ctypes.byref(record),
+            None if sc is None else ctypes.byref(sc), ctypes.c_void_p(stream or 0)))
+        del keep
 
     def integrate(self, params, solver, q, p, n_steps, f_pos=False, return_status=False):
         """n_steps steps of integrator `solver` (SOLVER_*); returns new (q, p)."""

@@ -603,9 +603,14 @@ class multi_gym(base_class):
         return q, p, factor
 
     def run_RHMC_batched(self, q_model_0, f_pos=True, delta=1e-6, Niter=100, Nsteps=100,
-                         dt=1e-1, counter_max=1000, rng="numpy", seeds=None, seed=0):
+                         dt=1e-1, counter_max=1000, rng="numpy", seeds=None, seed=0,
+                         schedule_g_ff2=None, schedule_beta=None):
         """Many independent chains of run_RHMC's move-0 loop, entirely on the GPU
         (rhmc_mh): Niter+1 MH iterations of Nsteps fused leapfrog steps.
+        schedule_g_ff2 / schedule_beta: run_RHMC's schedules
+        (sampler_RHMC.py:1010-1016) — iteration l runs with schedule[l] while l
+        < its size, then with its last value; afterwards self.g_ff2 / self.beta
+        hold the last value applied, as after run_RHMC.
 
         q_model_0: [n_chains, K, 3] (mag, x, y) or [K, 3] (one chain).
         rng="numpy": host randoms in the reference's per-iteration order
@@ -640,7 +645,11 @@ class multi_gym(base_class):
             raise ValueError("rng must be 'numpy' or 'device'")
         self._check_geometry()
         out = self._context().mh(self._params(delta, counter_max, for_energy=True), q0, n_iter,
-                                 Nsteps, f_pos=f_pos, z=z, u=u, seed=seed, record=True)
+                                 Nsteps, f_pos=f_pos, z=z, u=u, seed=seed, record=True,
+                                 schedule_g_ff2=schedule_g_ff2, schedule_beta=schedule_beta)
+        for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):
+            if sched is not None and np.size(sched) > 0:        # :1010-1016
+                setattr(self, name, float(np.ravel(sched)[min(n_iter, np.size(sched)) - 1]))
         self.q_chain, self.E_chain = out["q_chain"], out["E_chain"]
         self.V_chain, self.T_chain = out["V_chain"], out["T_chain"]
         self.A_chain = out["accept"].astype(bool)

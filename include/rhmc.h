@@ -25,6 +25,8 @@
  *       momentum draw p = z*sqrt(H(q)) (:1021-1022), E0 = V + T (:1025-1027),
  *       Nsteps leapfrog steps (:1053-1054), E1, accept if dE < 0 or
  *       ln u < -dE (:1072-1083) — n_iter iterations, all on the device.
+ *       rhmc_mh_scheduled(_device): the same with run_RHMC's schedule_g_ff2 /
+ *       schedule_beta (:1010-1016).
  *   rhmc_integrate / rhmc_integrate_device
  *       the reference's other integrators, selected by RHMC_SOLVER_*:
  *       single_gym.run_single_HMC leapfrog (sampler_RHMC.py:628-645) and
@@ -65,7 +67,7 @@
 extern "C" {
 #endif
 
-#define RHMC_ABI_VERSION 2
+#define RHMC_ABI_VERSION 3
 
 enum {
   RHMC_OK = 0,
@@ -274,6 +276,31 @@ int rhmc_mh(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains, in
 int rhmc_mh_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n_chains,
                    int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* d_z,
                    const double* d_u, uint64_t seed, const rhmc_mh_record* rec, void* stream);
+
+/*
+ * Parameter schedules of multi_gym.run_RHMC (schedule_g_ff2 / schedule_beta,
+ * sampler_RHMC.py:937-939, :1010-1016; RHMC-big-sim3.py:11-12): MH iteration
+ * l of the call runs with g_ff2 = g_ff2[l] and beta = beta[l] while l < the
+ * array's size, and with its last value after it; a NULL array (size 0)
+ * keeps P's value.  Host arrays, for the device entry point too (they set
+ * each iteration's constants).  P->g_ff2 / P->beta are not modified.
+ */
+typedef struct rhmc_mh_schedule {
+  const double* g_ff2;  /* [n_g_ff2] or NULL */
+  const double* beta;   /* [n_beta] or NULL  */
+  int32_t n_g_ff2;
+  int32_t n_beta;
+} rhmc_mh_schedule;
+/* rhmc_mh / rhmc_mh_device with a schedule (sched NULL: identical to them). */
+int rhmc_mh_scheduled(rhmc_ctx* ctx, const rhmc_params* P, double* q, int64_t n_chains,
+                      int32_t K, int32_t n_iter, int32_t n_steps, int32_t f_pos, const double* z,
+                      const double* u, uint64_t seed, const rhmc_mh_record* rec,
+                      const rhmc_mh_schedule* sched);
+int rhmc_mh_scheduled_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
+                             int64_t n_chains, int32_t K, int32_t n_iter, int32_t n_steps,
+                             int32_t f_pos, const double* d_z, const double* d_u, uint64_t seed,
+                             const rhmc_mh_record* rec, const rhmc_mh_schedule* sched,
+                             void* stream);
 
 /*
  * Data generation.  q: [K][3] (flux in counts, x, y), K >= 0.  n_real == 0:

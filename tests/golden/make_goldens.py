@@ -461,6 +461,51 @@ def case_mh(S, U):
     return out
 
 
+def case_mh_sched(S, U):
+    """multi_gym.run_RHMC with parameter schedules (sampler_RHMC.py:1010-1016):
+    iteration l sets g_ff2 = schedule_g_ff2[l] / beta = schedule_beta[l]
+    while l < the schedule's size, then keeps the last value — as in
+    RHMC-big-sim3.py (gff2_list = scheduler(1/5.**2, 4., 1000), beta_list =
+    scheduler(1e-5, 1e-7, 1000), utils.py:649-660).  The schedules here are
+    shorter than Niter + 1 so that the hold-the-last-value rule is exercised."""
+    out = {}
+    for name, stars_t, stars_m, kw, niter, nsteps, dt, vc in [
+        ("g1", [[19., 16.2, 15.7]], [[19.5, 16.6, 15.2]], dict(), 20, 10, 0.05, False),
+        ("g3", [[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4], [19.6, 15.3, 24.6]],
+         dict(g_xx=0.05, g_ff=4., g_ff2=4., prior=True), 20, 10, 0.01, False),
+        ("g3vc", [[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]],
+         [[18.3, 10.5, 12.2], [19.4, 20.0, 18.4], [19.6, 15.3, 24.6]],
+         dict(g_xx=0.05, g_ff=4., g_ff2=4., prior=True), 20, 10, 0.01, True),
+    ]:
+        np.random.seed(77)
+        g = make_gym(S, n=32, **kw)
+        g.gen_mock_data(np.array(stars_t))
+        sg = U.scheduler(1 / 5. ** 2, 4., 15)
+        sb = None
+        if vc:
+            g.use_Vc = True
+            g.beta = 1.
+            g.Vc_r_pow = 4.
+            g.f_expnt = np.zeros(len(stars_m))
+            sb = U.scheduler(1e-1, 1e-3, 12)
+        np.random.seed(321)
+        with contextlib.redirect_stdout(io.StringIO()):
+            g.run_RHMC(np.array(stars_m), f_pos=True, delta=1e-6, Niter=niter,
+                       Nsteps=nsteps, dt=dt, N_max=len(stars_m), schedule_g_ff2=sg,
+                       schedule_beta=sb)
+        res = dict(D=g.D, q_model=np.array(stars_m), q_chain=g.q_chain,
+                   p_chain=g.p_chain, E_chain=g.E_chain, V_chain=g.V_chain,
+                   T_chain=g.T_chain, A_chain=g.A_chain.astype(np.int32),
+                   niter=niter, nsteps=nsteps, seed=321, dt=dt, schedule_g_ff2=sg,
+                   schedule_beta=np.zeros(0) if sb is None else sb,
+                   g_ff2_final=g.g_ff2, beta_final=g.beta)
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+        print(name, "accepted", g.A_chain.sum(), "of", niter + 1)
+    return out
+
+
 # ----------------------------------------------------------------------------
 # Case 5: alternative integrators (single_gym, sampler_RHMC.py:592-783) and
 #         post-processing (utils.py:86-209)
@@ -646,7 +691,7 @@ def main():
     S, U, L, tmp = load_reference(args.ref)
     try:
         jobs = {"functions": case_functions, "steps": case_steps,
-                "mh": case_mh, "solvers": case_solvers,
+                "mh": case_mh, "mh_sched": case_mh_sched, "solvers": case_solvers,
                 "datagen": case_datagen}
         for name, fn in jobs.items():
             if args.only and args.only != name:

@@ -197,3 +197,79 @@ def test_run_RHMC_reversible_jump_moves(gpu_lib, name):
     assert_state_close(g.q_chain, z[name + "/q_chain"], 1e-9, "q_chain")
     assert_state_close(g.p_chain, z[name + "/p_chain"], 1e-9, "p_chain")
     np.testing.assert_allclose(g.E_chain, z[name + "/E_chain"], rtol=1e-11)
+
+
+def _sched_gym(z, name):
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    if par["use_Vc"]:
+        g.use_Vc, g.Vc_r_pow = True, par["Vc_r_pow"]
+        g.f_expnt = np.zeros(z[name + "/q_model"].shape[0])
+    sg = z[name + "/schedule_g_ff2"]
+    sb = z[name + "/schedule_beta"]
+    return g, sg, (sb if sb.size else None)
+
+
+@pytest.mark.parametrize("name", ["g1", "g3", "g3vc"])
+def test_run_RHMC_schedules_reproduce_reference(gpu_lib, name):
+    """run_RHMC with schedule_g_ff2 (and schedule_beta with repulsion),
+    sampler_RHMC.py:1010-1016 — the schedules are shorter than the run, so the
+    hold-the-last-value rule is exercised."""
+    z = load_golden("mh_sched")
+    g, sg, sb = _sched_gym(z, name)
+    np.random.seed(int(z[name + "/seed"]))
+    g.run_RHMC(z[name + "/q_model"].copy(), f_pos=True, delta=1e-6,
+               Niter=int(z[name + "/niter"]), Nsteps=int(z[name + "/nsteps"]),
+               dt=float(z[name + "/dt"]), N_max=z[name + "/q_model"].shape[0],
+               schedule_g_ff2=sg, schedule_beta=sb)
+    np.testing.assert_array_equal(g.A_chain.astype(np.int32), z[name + "/A_chain"])
+    assert_state_close(g.q_chain, z[name + "/q_chain"], 1e-9, "q_chain")
+    np.testing.assert_allclose(g.E_chain, z[name + "/E_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.V_chain, z[name + "/V_chain"], rtol=1e-11)
+    assert g.g_ff2 == z[name + "/g_ff2_final"] and g.beta == z[name + "/beta_final"]
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("name", ["g1", "g3", "g3vc"])
+def test_run_RHMC_batched_schedules_reproduce_reference(gpu_lib, monkeypatch, name, fused):
+    """The on-device MH loop (rhmc_mh_scheduled) with the reference's NumPy
+    draws and its schedules reproduces the reference chain — on the fused
+    one-star kernel (one launch per iteration under a schedule), the fused
+    multi-star kernel and the four-kernel loop (fused=False, and g3vc: the
+    repulsion re-evaluates V(q) per iteration under a beta schedule)."""
+    from rhmc_amd import capi
+    monkeypatch.setattr(capi, "DEFAULT_MH_FUSED", fused)
+    z = load_golden("mh_sched")
+    g, sg, sb = _sched_gym(z, name)
+    np.random.seed(int(z[name + "/seed"]))
+    g.run_RHMC_batched(z[name + "/q_model"].copy(), f_pos=True, Niter=int(z[name + "/niter"]),
+                       Nsteps=int(z[name + "/nsteps"]), dt=float(z[name + "/dt"]),
+                       schedule_g_ff2=sg, schedule_beta=sb)
+    np.testing.assert_array_equal(g.A_chain[:, 0].astype(np.int32), z[name + "/A_chain"])
+    K3 = g.q_chain.shape[2]
+    assert_state_close(g.q_chain[:, 0], z[name + "/q_chain"][:, :K3], 1e-9, "q_chain")
+    np.testing.assert_allclose(g.E_chain[:, 0], z[name + "/E_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.V_chain[:, 0], z[name + "/V_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.T_chain[:, 0], z[name + "/T_chain"], rtol=1e-10, atol=1e-10)
+    assert g.g_ff2 == z[name + "/g_ff2_final"] and g.beta == z[name + "/beta_final"]
+
+
+@pytest.mark.parametrize("name", ["g1", "g3"])
+def test_mh_constant_schedule_equals_unscheduled_run(gpu_lib, name):
+    """A one-entry schedule (held for every iteration) equals the unscheduled
+    run at that g_ff2, bit for bit, with device randoms: the scheduled path
+    (one launch per iteration, Philox keyed by the run's iteration index,
+    V(q) re-evaluated per launch) changes nothing but the constants."""
+    z = load_golden("mh_sched")
+    g, sg, _ = _sched_gym(z, name)
+    g.dt = 0.02
+    qm = np.stack([z[name + "/q_model"]] * 6).reshape(6, -1).copy()
+    qm[:, 0::3] = g.mag2flux_converter(qm[:, 0::3])
+    g.g_ff2 = sg[0]
+    a = g._context().mh(g._params(for_energy=True), qm, 5, 6, seed=4, record=True)
+    g.g_ff2 = 123.0            # overridden by the schedule in every iteration
+    b = g._context().mh(g._params(for_energy=True), qm, 5, 6, seed=4, record=True,
+                        schedule_g_ff2=np.array([sg[0]]))
+    for k in ("q", "accept", "E_chain", "V_chain", "T_chain", "q_chain"):
+        assert np.array_equal(a[k], b[k]), k
