@@ -37,6 +37,7 @@
 #include "rhmc_pixk.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
+#include "rhmc_dense.hpp"
 
 namespace rhmc {
 
@@ -515,22 +516,19 @@ __device__ __forceinline__ void run_steps_win(WinState<SLOTS>& s, int n_steps, i
   }
 }
 
-template <int SLOTS>
-__device__ __forceinline__ WinTables win_tables(double* lds, int K) {
-  double* base_tab = lds + (threadIdx.x / kWave) * win_table_doubles(K);
-  return WinTables{base_tab, base_tab + K * kTabW};
-}
 
-// Windowed leapfrog (any square image, 1 <= K <= 64 SLOTS): D from global memory.
-template <int SLOTS>
+// Leapfrog on the slotted state (1 <= K <= 64 SLOTS) with gradient policy G:
+// WinG (windowed, any square image, D from global memory) or DenseG<IMG>
+// (rhmc_dense.hpp: 32/48-px images, many stars).
+template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
   extern __shared__ double lds[];
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
   WinState<SLOTS> s;
   win_load<SLOTS>(a, chain, K, s);
@@ -541,7 +539,7 @@ __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
       s, a.n_steps, rows, cols, c, it_p, it_q, st,
       [&](const double(&f)[SLOTS], const double(&x)[SLOTS], const double(&y)[SLOTS],
           double(&gf)[SLOTS], double(&gx)[SLOTS], double(&gy)[SLOTS]) {
-        win_gradient<SLOTS>(a.D, tab, K, f, x, y, rows, cols, c, lc, true, gf, gx, gy);
+        G::template gradient<SLOTS>(gctx, K, f, x, y, c, lc, true, gf, gx, gy);
       });
   win_store<SLOTS>(a, chain, K, s, it_p, it_q, st);
 }
@@ -687,19 +685,18 @@ __device__ __forceinline__ double dVdq_rhmc_f(double f, double pf, const Consts&
   return (t1 + t2) / 2.0;
 }
 
-template <int SOLVER, int SLOTS>
+template <class G, int SOLVER, int SLOTS>
 __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_pos) {
   extern __shared__ double lds[];
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
   WinState<SLOTS> s;
   win_load<SLOTS>(a, chain, K, s);
-  const int rows = a.g.rows, cols = a.g.cols;
   const double dt = c.dt;
   unsigned st = 0u;
   double gf[SLOTS], gx[SLOTS], gy[SLOTS];
@@ -709,7 +706,7 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
   // next step's first one (same q).
   for (int step = 0;; ++step) {
     if (SOLVER == RHMC_SOLVER_RHMC_NAIVE && step == a.n_steps) break;
-    win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+    G::template gradient<SLOTS>(gctx, K, s.f, s.x, s.y, c, lc, false, gf, gx, gy);
     if (SOLVER == RHMC_SOLVER_RHMC_NAIVE) {  // :690-708, the gradient at the step's start
 #pragma unroll
       for (int t = 0; t < SLOTS; ++t) {
@@ -785,22 +782,21 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
 // last step flipped, p_tmp keeps the momentum the trajectory started from
 // (:547-550 update p_half, not p_tmp) — status bit RHMC_STATUS_REFLECT_F
 // marks those chains.  One wave per chain, star 64 s + lane in slot s.
-template <int SLOTS>
+template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
                                                              const double* __restrict__ dtv,
                                                              const int32_t* __restrict__ steps) {
   extern __shared__ double lds[];
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
   const int lane = lane_id();
   WinState<SLOTS> s;
   win_load<SLOTS>(a, chain, K, s);
-  const int rows = a.g.rows, cols = a.g.cols;
   double dtf[SLOTS], dtx[SLOTS], dty[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
@@ -810,7 +806,7 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
     dty[t] = dtv[3 * ks + 2];
   }
   double gf[SLOTS], gx[SLOTS], gy[SLOTS];
-  win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+  G::template gradient<SLOTS>(gctx, K, s.f, s.x, s.y, c, lc, false, gf, gx, gy);
   double hf[SLOTS], hx[SLOTS], hy[SLOTS];
   bool iflip[SLOTS];
 #pragma unroll
@@ -834,7 +830,7 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
       below_any = below_any || below;
     }
     flip = __builtin_amdgcn_ballot_w64(below_any) != 0;
-    win_gradient<SLOTS>(a.D, tab, K, s.f, s.x, s.y, rows, cols, c, lc, false, gf, gx, gy);
+    G::template gradient<SLOTS>(gctx, K, s.f, s.x, s.y, c, lc, false, gf, gx, gy);
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) {
       const double kept = -hf[t];                                       // :531
@@ -874,20 +870,19 @@ __device__ __forceinline__ void win_load_q(const double* q, int64_t chain, int K
 }
 
 // Large-image gradient (windowed), one wave per chain.
-template <int SLOTS>
+template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   extern __shared__ double lds[];
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int K = a.K;
-  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(a.c);
   double f[SLOTS], x[SLOTS], y[SLOTS], gf[SLOTS], gx[SLOTS], gy[SLOTS];
   bool own[SLOTS];
   win_load_q<SLOTS>(a.q, chain, K, f, x, y, own);
-  win_gradient<SLOTS>(a.D, tab, K, f, x, y, a.g.rows, a.g.cols, a.c, lc, a.with_metric != 0,
-                      gf, gx, gy);
+  G::template gradient<SLOTS>(gctx, K, f, x, y, a.c, lc, a.with_metric != 0, gf, gx, gy);
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
     if (!own[t]) continue;
@@ -899,9 +894,10 @@ __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
 }
 
 // Large-image V and T (windowed tables, pixel-major V).
-template <int SLOTS>
+template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   extern __shared__ double lds[];
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
   const Geometry& g = a.g;
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
@@ -909,7 +905,6 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   if (chain >= a.n_chains) return;
   const int lane = lane_id();
   const int K = a.K;
-  const WinTables tab = win_tables<SLOTS>(lds, K);
   const LeanConsts lc = lean_consts(c);
   double f[SLOTS], x[SLOTS], y[SLOTS];
   bool own[SLOTS];
@@ -944,7 +939,7 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
     if (lane == 0) a.V[chain] = INFINITY;
     return;
   }
-  double v = win_potential<SLOTS>(a.D, tab, K, f, x, y, g.rows, g.cols, c, lc);
+  double v = G::template potential<SLOTS>(gctx, K, f, x, y, c, lc);
   if (c.use_prior) {
     double vp = 0.0;
 #pragma unroll
@@ -1042,17 +1037,40 @@ constexpr int kMaxK = 256;         // windowed kernels: 64 lanes x 4 star slots
 // Star slots per lane of the windowed kernels for K stars.
 int win_slots(int K) { return K <= 64 ? 1 : (K <= 128 ? 2 : 4); }
 
-template <int SLOTS>
+template <class G, int SLOTS>
 void launch_integrate_win(int32_t solver, dim3 grid, dim3 block, size_t lds, hipStream_t s,
                           const LeapArgs& a, int fp) {
   if (solver == RHMC_SOLVER_HMC)
-    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_HMC, SLOTS>), grid, block, lds, s, a, fp);
+    hipLaunchKernelGGL((integrate_win_kernel<G, RHMC_SOLVER_HMC, SLOTS>), grid, block, lds, s, a,
+                       fp);
   else if (solver == RHMC_SOLVER_RHMC_NAIVE)
-    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_RHMC_NAIVE, SLOTS>), grid, block, lds, s,
-                       a, fp);
-  else
-    hipLaunchKernelGGL((integrate_win_kernel<RHMC_SOLVER_RHMC_LEAPFROG, SLOTS>), grid, block, lds,
+    hipLaunchKernelGGL((integrate_win_kernel<G, RHMC_SOLVER_RHMC_NAIVE, SLOTS>), grid, block, lds,
                        s, a, fp);
+  else
+    hipLaunchKernelGGL((integrate_win_kernel<G, RHMC_SOLVER_RHMC_LEAPFROG, SLOTS>), grid, block,
+                       lds, s, a, fp);
+}
+
+// The slotted one-wave-per-chain kernels run one of two gradient policies:
+// WinG (windowed tables, any square image; needs window_exact) or DenseG<IMG>
+// (rhmc_dense.hpp, 32/48-px images: full-image pixel-major Lambda, star-major
+// sums).  A "path" names it: 0 = windowed, 32 / 48 = dense at that side.
+template <class T> struct TypeTag { using type = T; };
+template <int N> struct IntTag { static constexpr int value = N; };
+
+template <class G, class F>
+int with_slots(int K, F&& f) {
+  switch (win_slots(K)) {
+    case 1: return f(TypeTag<G>{}, IntTag<1>{});
+    case 2: return f(TypeTag<G>{}, IntTag<2>{});
+    default: return f(TypeTag<G>{}, IntTag<4>{});
+  }
+}
+template <class F>
+int with_path(int path, int K, F&& f) {
+  if (path == 32) return with_slots<DenseG<32>>(K, f);
+  if (path == 48) return with_slots<DenseG<48>>(K, f);
+  return with_slots<WinG>(K, f);
 }
 
 // Which kernel family serves (K, image): the LDS-image kernels need D and the
@@ -1071,6 +1089,43 @@ void pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
   while (w > 1 && w * per > (size_t)ctx->max_lds) w >>= 1;
   *W = w;
   *lds = w * per;  // K <= 256: 135 KB for one wave, within the CU's 160 KB
+}
+
+// The slotted kernels' workgroup for a path (with_path): the windowed tables'
+// LDS as above, or four waves of the dense kernel (32 px: 41.5 KB, 48 px:
+// 92.6 KB).
+void pick_waves_path(const rhmc_ctx* ctx, int path, int K, size_t* lds, int* W) {
+  if (path == 32 || path == 48) {
+    *W = 4;
+    *lds = path == 32 ? DenseG<32>::lds_bytes(4) : DenseG<48>::lds_bytes(4);
+    return;
+  }
+  pick_waves_win(ctx, K, lds, W);
+}
+
+// The dense many-star kernel (rhmc_dense.hpp) for (K, image): by default from
+// kDenseMinK stars on 32/48-px square images (where every star's window
+// covers most of the image); RHMC_KERNEL_DENSE forces it on those images at
+// any K, GENERIC / WINDOWED keep the per-wave families, MULTIWIN(_NOTAB)
+// keeps the multi-star register-window kernel where it applies (K <= 64).
+// Measured against the multi-star register-window kernel (4096 chains, 100
+// steps, chain-steps/s, profiles/r04_dense/): 32 px K = 12 6.7e7 vs 7.5e7,
+// K = 16 6.6e7 vs 5.0e7, K = 24 5.6e7 vs 1.6e7; 48 px K = 12 2.6e7 vs 4.5e7,
+// K = 16 2.6e7 vs 2.6e7, K = 24 2.4e7 vs 1.6e7, K = 40 2.2e7 vs 6.3e6;
+// big-sim4 (32 px, K = 51) 4.2e7 vs 3.7e6, big-sim3 (K = 100) 2.2e7 vs 1.7e5
+// for the windowed kernel.
+constexpr int kDenseMinK = 16;
+bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c);
+int dense_path(const rhmc_ctx* ctx, int K, const Consts& c) {
+  if (ctx->rows != ctx->cols || (ctx->rows != 32 && ctx->rows != 48)) return 0;
+  if (per_wave_forced(ctx)) return 0;
+  if (ctx->kernel != RHMC_KERNEL_DENSE) {
+    if (K < kDenseMinK) return 0;
+    if ((ctx->kernel == RHMC_KERNEL_MULTIWIN || ctx->kernel == RHMC_KERNEL_MULTIWIN_NOTAB) &&
+        tiledrk_ok(ctx, K, c))
+      return 0;
+  }
+  return ctx->rows;
 }
 
 Geometry make_geometry(int rows, int cols) {
@@ -1320,7 +1375,8 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   // (rhmc_mhk1.hpp); RHMC_KERNEL_GENERIC / _WINDOWED keep the per-wave kernels
   const int side = ctx->rows;
   if (K == 1 && !c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
-      reg_window_ok(28, c.inv_two_sig2) && !per_wave_forced(ctx)) {
+      reg_window_ok(28, c.inv_two_sig2) && !per_wave_forced(ctx) &&
+      ctx->kernel != RHMC_KERNEL_DENSE) {
     if (n == 0) return RHMC_OK;
     EnergyK1Args k;
     k.q = d_q;
@@ -1344,10 +1400,11 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   size_t lds;
   int W;
   int rc;
-  const bool win = use_windowed(ctx, K);
-  if (win && !window_exact(c)) return window_unsupported();
+  const int path = dense_path(ctx, K, c);
+  const bool win = path || use_windowed(ctx, K);
+  if (win && !path && !window_exact(c)) return window_unsupported();
   if (win)
-    pick_waves_win(ctx, K, &lds, &W);
+    pick_waves_path(ctx, path, K, &lds, &W);
   else if ((rc = pick_waves(ctx, K, &lds, &W)))
     return rc;
   a.q = d_q;
@@ -1361,13 +1418,12 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
-    switch (win_slots(K)) {
-      case 1: hipLaunchKernelGGL(energy_win_kernel<1>, grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL(energy_win_kernel<2>, grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL(energy_win_kernel<4>, grid, block, lds, s, a); break;
-    }
-    HIP_TRY(hipGetLastError());
-    return RHMC_OK;
+    return with_path(path, K, [&](auto gt, auto st) {
+      using G = typename decltype(gt)::type;
+      hipLaunchKernelGGL((energy_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a);
+      HIP_TRY(hipGetLastError());
+      return (int)RHMC_OK;
+    });
   }
   return dispatch_k<EnergyLaunch>(K, grid, block, lds, s, a);
 }
@@ -1458,7 +1514,7 @@ int launch_kr(const rhmc_ctx* ctx, LeapArgsKR a, int f_pos, hipStream_t s) {
 bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
   const int k = ctx->kernel;
   const bool want = !per_wave_forced(ctx) && k != RHMC_KERNEL_MULTIWIN &&
-                    k != RHMC_KERNEL_MULTIWIN_NOTAB;
+                    k != RHMC_KERNEL_MULTIWIN_NOTAB && k != RHMC_KERNEL_DENSE;
   return want && K >= 2 && K <= 10 && !c.use_Vc && ctx->img_f32 && ctx->rows == ctx->cols &&
          (ctx->rows == 32 || ctx->rows == 48);
 }
@@ -1498,7 +1554,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   // one star: the register-window kernel (C1, C2) or, from 16 Ki chains, the
   // lane-group kernel (C4 shards); wider PSFs and other image sides take the
   // generic kernel below
-  const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !per_wave_forced(ctx);
+  const bool k1 = K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !per_wave_forced(ctx) &&
+                  ctx->kernel != RHMC_KERNEL_DENSE;
   const bool img_ok = side == 32 || side == 48 || side == 64 || side == 96 || side == 128;
   if (k1 && img_ok && reg_window_ok(32, a.c.inv_two_sig2)) {
     LeapArgsK1 t;
@@ -1530,7 +1587,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
       default: return launch_tiledr<128>(ctx, t, s);
     }
   }
-  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
+  const int path = dense_path(ctx, K, a.c);
+  if (!path && (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c))) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -1552,8 +1610,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
-  if (use_windowed(ctx, K)) {
-    if (!window_exact(a.c)) return window_unsupported();
+  if (path || use_windowed(ctx, K)) {
+    if (!path && !window_exact(a.c)) return window_unsupported();
     a.q = d_q;
     a.p = d_p;
     a.fp_iters = d_it;
@@ -1562,15 +1620,14 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.n_chains = n_chains;
     a.K = K;
     a.n_steps = n_steps;
-    pick_waves_win(ctx, K, &lds, &W);
+    pick_waves_path(ctx, path, K, &lds, &W);
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
-    switch (win_slots(K)) {
-      case 1: hipLaunchKernelGGL(leapfrog_win_kernel<1>, grid, block, lds, s, a); break;
-      case 2: hipLaunchKernelGGL(leapfrog_win_kernel<2>, grid, block, lds, s, a); break;
-      default: hipLaunchKernelGGL(leapfrog_win_kernel<4>, grid, block, lds, s, a); break;
-    }
-    HIP_TRY(hipGetLastError());
-    return RHMC_OK;
+    return with_path(path, K, [&](auto gt, auto st) {
+      using G = typename decltype(gt)::type;
+      hipLaunchKernelGGL((leapfrog_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a);
+      HIP_TRY(hipGetLastError());
+      return (int)RHMC_OK;
+    });
   }
   a.q = d_q;
   a.p = d_p;
@@ -1871,7 +1928,8 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   // / _WINDOWED keep the windowed one)
   const int side = ctx->rows;
   if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && !per_wave_forced(ctx) &&
-      (side == 32 || side == 48 || side == 64) && reg_window_ok(28, a.c.inv_two_sig2)) {
+      ctx->kernel != RHMC_KERNEL_DENSE && (side == 32 || side == 48 || side == 64) &&
+      reg_window_ok(28, a.c.inv_two_sig2)) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -1894,8 +1952,10 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
     }
   }
   // many stars: the pixel-major kernel (full image, any PSF width) or the
-  // multi-star register-window kernel (rhmc_tiledrk.hpp, 28-px windows)
-  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
+  // multi-star register-window kernel (rhmc_tiledrk.hpp, 28-px windows);
+  // many stars on a small image: the dense kernel (below)
+  const int path = dense_path(ctx, K, a.c);
+  if (!path && (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c))) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -1923,7 +1983,7 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
     if (solver == RHMC_SOLVER_RHMC_NAIVE) return launch_kr<RHMC_SOLVER_RHMC_NAIVE>(ctx, t, fp, s);
     return launch_kr<RHMC_SOLVER_RHMC_LEAPFROG>(ctx, t, fp, s);
   }
-  if (!window_exact(a.c)) return window_unsupported();  // integrate_win_kernel
+  if (!path && !window_exact(a.c)) return window_unsupported();  // integrate_win_kernel
   a.q = d_q;
   a.p = d_p;
   a.fp_iters = nullptr;
@@ -1935,17 +1995,16 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
-  pick_waves_win(ctx, K, &lds, &W);
+  pick_waves_path(ctx, path, K, &lds, &W);
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
-  switch (win_slots(K)) {
-    case 1: launch_integrate_win<1>(solver, grid, block, lds, s, a, fp); break;
-    case 2: launch_integrate_win<2>(solver, grid, block, lds, s, a, fp); break;
-    default: launch_integrate_win<4>(solver, grid, block, lds, s, a, fp); break;
-  }
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
+  return with_path(path, K, [&](auto gt, auto st) {
+    launch_integrate_win<typename decltype(gt)::type, decltype(st)::value>(solver, grid, block,
+                                                                          lds, s, a, fp);
+    HIP_TRY(hipGetLastError());
+    return (int)RHMC_OK;
+  });
 }
 
 template <int IMG>
@@ -1980,7 +2039,8 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   // / _WINDOWED keep the windowed one)
   const int side = ctx->rows;
   if (K == 1 && !a.c.use_Vc && ctx->rows == ctx->cols && (side == 32 || side == 48 || side == 64) &&
-      reg_window_ok(28, a.c.inv_two_sig2) && !per_wave_forced(ctx)) {
+      reg_window_ok(28, a.c.inv_two_sig2) && !per_wave_forced(ctx) &&
+      ctx->kernel != RHMC_KERNEL_DENSE) {
     LeapArgsK1 t;
     t.q = d_q;
     t.p = d_p;
@@ -2003,8 +2063,10 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   }
   // many stars: the pixel-major kernel (full image, any PSF width) or the
   // multi-star register-window kernel (rhmc_tiledrk.hpp); RHMC_KERNEL_MULTIWIN
-  // forces the latter, GENERIC / WINDOWED the windowed kernel below.
-  if (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c)) {
+  // forces the latter, GENERIC / WINDOWED the windowed kernel below; many
+  // stars on a small image: the dense kernel (below)
+  const int path = dense_path(ctx, K, a.c);
+  if (!path && (use_pixk(ctx, K, a.c) || use_tiledrk(ctx, K, a.c))) {
     LeapArgsKR t;
     t.q = d_q;
     t.p = d_p;
@@ -2024,7 +2086,7 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
     if (use_pixk(ctx, K, a.c)) return launch_pk_side<kSolverHmcRandom>(ctx, t, s, 0);
     return launch_kr<kSolverHmcRandom>(ctx, t, 0, s);
   }
-  if (!window_exact(a.c)) return window_unsupported();  // windowed gradient
+  if (!path && !window_exact(a.c)) return window_unsupported();  // windowed gradient
   a.q = d_q;
   a.p = d_p;
   a.fp_iters = nullptr;
@@ -2036,16 +2098,16 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
-  pick_waves_win(ctx, K, &lds, &W);
+  pick_waves_path(ctx, path, K, &lds, &W);
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
-  switch (win_slots(K)) {
-    case 1: hipLaunchKernelGGL(hmc_random_win_kernel<1>, grid, block, lds, s, a, d_dt, d_steps); break;
-    case 2: hipLaunchKernelGGL(hmc_random_win_kernel<2>, grid, block, lds, s, a, d_dt, d_steps); break;
-    default: hipLaunchKernelGGL(hmc_random_win_kernel<4>, grid, block, lds, s, a, d_dt, d_steps); break;
-  }
-  HIP_TRY(hipGetLastError());
-  return RHMC_OK;
+  return with_path(path, K, [&](auto gt, auto st) {
+    using G = typename decltype(gt)::type;
+    hipLaunchKernelGGL((hmc_random_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a,
+                       d_dt, d_steps);
+    HIP_TRY(hipGetLastError());
+    return (int)RHMC_OK;
+  });
 }
 
 // Model image / Poisson realisations (rhmc_datagen.hpp) into d_out
@@ -2194,7 +2256,7 @@ int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   switch (option) {
     case RHMC_OPT_KERNEL:
-      if (value < RHMC_KERNEL_AUTO || value > RHMC_KERNEL_MULTIWIN_NOTAB)
+      if (value < RHMC_KERNEL_AUTO || value > RHMC_KERNEL_DENSE)
         return fail(RHMC_ERR_ARG, "unknown RHMC_KERNEL_* value " + std::to_string(value));
       ctx->kernel = value;
       return RHMC_OK;
@@ -2297,10 +2359,11 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   if ((rc = make_consts(P, &a.c))) return rc;
   size_t lds;
   int W;
-  const bool win = use_windowed(ctx, K);
-  if (win && !window_exact(a.c)) return window_unsupported();
+  const int path = dense_path(ctx, K, a.c);
+  const bool win = path || use_windowed(ctx, K);
+  if (win && !path && !window_exact(a.c)) return window_unsupported();
   if (win)
-    pick_waves_win(ctx, K, &lds, &W);
+    pick_waves_path(ctx, path, K, &lds, &W);
   else if ((rc = pick_waves(ctx, K, &lds, &W)))
     return rc;
   const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
@@ -2318,12 +2381,14 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
-    switch (win_slots(K)) {
-      case 1: hipLaunchKernelGGL(gradient_win_kernel<1>, grid, block, lds, ctx->stream, a); break;
-      case 2: hipLaunchKernelGGL(gradient_win_kernel<2>, grid, block, lds, ctx->stream, a); break;
-      default: hipLaunchKernelGGL(gradient_win_kernel<4>, grid, block, lds, ctx->stream, a); break;
-    }
-    HIP_TRY(hipGetLastError());
+    rc = with_path(path, K, [&](auto gt, auto st) {
+      using G = typename decltype(gt)::type;
+      hipLaunchKernelGGL((gradient_win_kernel<G, decltype(st)::value>), grid, block, lds,
+                         ctx->stream, a);
+      HIP_TRY(hipGetLastError());
+      return (int)RHMC_OK;
+    });
+    if (rc) return rc;
   } else if ((rc = dispatch_k<GradLaunch>(K, grid, block, lds, ctx->stream, a))) {
     return rc;
   }

@@ -279,4 +279,44 @@ __device__ double win_potential(const double* __restrict__ D, const WinTables& t
   return wave_sum_dpp(v);
 }
 
+// Gradient policy of the slotted kernels (rhmc_kernels.hip) on windowed
+// tables: any square image, D read from global memory (L2).
+struct WinG {
+  static __host__ __device__ size_t lds_bytes(int waves, int K) {
+    return (size_t)waves * win_table_doubles(K) * sizeof(double);
+  }
+  struct Ctx {
+    WinTables tab;
+    const double* D;
+    int rows, cols;
+  };
+  static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
+                                              int cols) {
+    double* base = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+    Ctx g;
+    g.tab = WinTables{base, base + K * kTabW};
+    g.D = D;
+    g.rows = rows;
+    g.cols = cols;
+    return g;
+  }
+  template <int SLOTS>
+  static __device__ __forceinline__ void gradient(const Ctx& g, int K, const double (&f)[SLOTS],
+                                                  const double (&x)[SLOTS],
+                                                  const double (&y)[SLOTS], const Consts& c,
+                                                  const LeanConsts& lc, bool with_metric,
+                                                  double (&gf)[SLOTS], double (&gx)[SLOTS],
+                                                  double (&gy)[SLOTS]) {
+    win_gradient<SLOTS>(g.D, g.tab, K, f, x, y, g.rows, g.cols, c, lc, with_metric, gf, gx, gy);
+  }
+  template <int SLOTS>
+  static __device__ __forceinline__ double potential(const Ctx& g, int K,
+                                                     const double (&f)[SLOTS],
+                                                     const double (&x)[SLOTS],
+                                                     const double (&y)[SLOTS], const Consts& c,
+                                                     const LeanConsts& lc) {
+    return win_potential<SLOTS>(g.D, g.tab, K, f, x, y, g.rows, g.cols, c, lc);
+  }
+};
+
 }  // namespace rhmc

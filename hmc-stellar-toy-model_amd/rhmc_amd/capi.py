@@ -34,7 +34,7 @@ OPT_WINDOW_SPLIT = 3        # waves per chain pair in leapfrog_kr (0: by batch s
 # RHMC_KERNEL_* values by name
 KERNELS = {"auto": 0, "generic": 1, "windowed": 2, "regwin": 3, "regwin32": 4,
            "regwin_f64": 5, "lane1": 6, "lane4": 7, "lane1_f64": 8, "pixmajor": 9,
-           "multiwin": 10, "multiwin_notab": 11}
+           "multiwin": 10, "multiwin_notab": 11, "dense": 12}
 # What a new Context selects unless told otherwise.  Production code leaves
 # these alone; the parity tests set them (monkeypatch) to run the same inputs
 # through every kernel family.  The library itself reads no environment.

@@ -6,10 +6,18 @@ Every config is a data image plus a batch of chain states (q0, p0):
   C3  48x48,  K=10, 16384 chains    (multi-source gradient)
   C4  48x48,  K=1,  2^20 chains     sharded over 8 GPUs
   C5  256x256, K=64, 8192 chains    (flux-wall RHMC, prior on)
+Beyond BASELINE's configs, the reference's own many-star drivers (dense
+32x32 images, big-sim4 parameters, prior on):
+  B4  32x32, K=51,  4096 chains, 100 steps (RHMC-big-sim4.py: 32**2 * 0.05 stars)
+  B3  32x32, K=100, 4096 chains, 100 steps (RHMC-big-sim3.py: Nobjs = 100)
+  S<n>K<k>  n x n, K=k, 4096 chains, 100 steps, the same parameters (kernel
+            sweeps, e.g. S48K32)
 
 Randomness: numpy legacy RandomState; the image uses seed 77
 (RHMC-big-sim4.py:18), chain initial states seed 1000 (+ shard offset).
 """
+import re
+
 import numpy as np
 
 from .photometry import (default_exp_setup, factors, gauss_PSF, gen_pow_law_sample,
@@ -80,10 +88,13 @@ def make(name, n_chains=None, seed_offset=0):
                            yt + 0.5 * rng.randn(nc)], 1)
         K = 1
         steps = 100 if name == "C1" else 500
-    elif name == "C3" or name == "C5":
-        n, K = (48, 10) if name == "C3" else (256, 64)
+    elif name in ("C3", "C5", "B3", "B4") or re.fullmatch(r"S\d+K\d+", name):
+        if name[0] == "S":
+            n, K = (int(v) for v in re.fullmatch(r"S(\d+)K(\d+)", name).groups())
+        else:
+            n, K = {"C3": (48, 10), "C5": (256, 64), "B3": (32, 100), "B4": (32, 51)}[name]
         par, ftc = base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.,
-                               use_prior=(name == "C5"), alpha=2.)
+                               use_prior=(name != "C3"), alpha=2.)
         if par["use_prior"]:
             # V's prior constant for the power-law flux range (sampler_RHMC.py:321)
             a = par["alpha"]
@@ -93,13 +104,13 @@ def make(name, n_chains=None, seed_offset=0):
         ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc)
         D = _image(n, [(22.5 - 2.5 * np.log10(a / ftc), b, c) for a, b, c in zip(ft, xt, yt)],
                    ftc, par["B_count"], par["fwhm_pix"], img_rng)
-        nc = (16384 if name == "C3" else 8192) if n_chains is None else n_chains
+        nc = ({"C3": 16384, "C5": 8192}.get(name, 4096)) if n_chains is None else n_chains
         # chains start at the truth, perturbed (flux x lognormal 10%, 0.5 px)
         q0 = np.empty((nc, 3 * K))
         q0[:, 0::3] = ft * np.exp(0.1 * rng.randn(nc, K))
         q0[:, 1::3] = xt + 0.5 * rng.randn(nc, K)
         q0[:, 2::3] = yt + 0.5 * rng.randn(nc, K)
-        steps = 500
+        steps = 500 if name[0] == "C" else 100
     else:
         raise ValueError("unknown workload " + name)
     H = metric_diag(q0, par)

@@ -141,6 +141,9 @@ typedef struct rhmc_ctx rhmc_ctx;
  *   MULTIWIN        K >= 2 multi-star register-window kernel (also where the
  *                   pixel-major kernel would serve); MULTIWIN_NOTAB without
  *                   the LDS factor tables
+ *   DENSE           the many-star kernel for 32/48-px images (full-image
+ *                   pixel-major Lambda, star-major sums; the AUTO choice there
+ *                   from 11 stars) at any K
  * RHMC_OPT_MH_FUSED: 1 (default) = one-launch MH where a fused kernel exists,
  *   0 = the four-kernel loop (begin / leapfrog / energy / end) always.
  * RHMC_OPT_WINDOW_SPLIT: waves per chain pair in the multi-star
@@ -170,7 +173,8 @@ enum {
   RHMC_KERNEL_LANE1_F64 = 8,
   RHMC_KERNEL_PIXMAJOR = 9,
   RHMC_KERNEL_MULTIWIN = 10,
-  RHMC_KERNEL_MULTIWIN_NOTAB = 11
+  RHMC_KERNEL_MULTIWIN_NOTAB = 11,
+  RHMC_KERNEL_DENSE = 12
 };
 int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value);
 int rhmc_ctx_get_option(rhmc_ctx* ctx, int32_t option, int32_t* value);

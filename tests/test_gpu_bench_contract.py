@@ -30,7 +30,10 @@ def test_bench_json_line():
     r = d["roofline"]
     for key in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel_ms"):
         assert key in r
-    assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+    if r["pmc_stale"]:            # PMC summary taken on other sources: no fraction
+        assert r["frac"] is None and r["achieved"] is None
+    else:
+        assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
     # value counts wall time around the launches, kernel_ms the launches alone
     assert d["ms_per_step"] >= 0.9 * r["kernel_ms"]
     assert d["nonfinite_chains"] == 0

@@ -2,7 +2,9 @@
 drivers run K = 100 (RHMC-big-sim3.py:18-19) and grow K by births up to
 N_max = 120 (RHMC-big-sim4.py:77); its dVdq / V / RHMC_single_step take any
 3 * Nobjs (sampler_RHMC.py:365-425, :294-351, :522-566).  The engine takes
-1 <= K <= 256.
+1 <= K <= 256.  Every test runs on the automatic choice (32/48-px images: the
+dense many-star kernel, rhmc_dense.hpp; 256 px: the windowed kernel) and
+with each family forced.
 
 Pinned by reference fixtures (tests/golden/make_goldens.py case_bigk):
 bigk.npz (dVdq, dphidq, V, T at K = 100 on 32x32 with prior and with
@@ -24,7 +26,7 @@ from oracle import rhmc_ref as R
 
 pytestmark = pytest.mark.gpu
 
-BIGK_KERNELS = ["auto", "windowed", "multiwin"]
+BIGK_KERNELS = ["auto", "windowed", "multiwin", "dense"]
 
 
 @pytest.fixture(params=BIGK_KERNELS)
@@ -272,6 +274,7 @@ def test_run_RHMC_births_past_64(gpu_lib):
     q = zb["Q"][0, 0][:3 * 64].copy()
     p = zb["P"][0, 0][:3 * 64].copy()
     g.Nobjs, g.d = 64, 192
+    g.V(q, f_pos=True)        # caches V_prior_const (:320-321), as run_RHMC's first V does
     np.random.seed(5)
     for _ in range(3):                                    # 64 -> 67 stars
         q, p, _ = g.birth_death_move(q, p, True)

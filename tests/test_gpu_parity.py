@@ -22,7 +22,7 @@ def _ctx(capi, z):
 
 
 KERNEL_PATHS = ["auto", "generic", "windowed", "multiwin", "multiwin_notab", "pixmajor",
-                "regwin", "regwin32", "regwin_f64", "lane1", "lane4", "lane1_f64"]
+                "regwin", "regwin32", "regwin_f64", "lane1", "lane4", "lane1_f64", "dense"]
 
 
 @pytest.fixture(params=KERNEL_PATHS)
