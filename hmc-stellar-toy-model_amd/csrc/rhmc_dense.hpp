@@ -18,12 +18,14 @@
 //       pixel-star and 2 BS LDS reads per BS^2 FMAs.
 //   pass 2   s = D / Lambda - 1 (:379), one v_rcp_f64 per four pixels,
 //       written to the wave's LDS region (over the tables).
-//   pass 3 (star-major)  lane = star: A0 = sum_ij ex(i) ey(j) s_ij,
+//   pass 3 (star-major)  lane = (star, row group): A0 = sum_ij ex(i) ey(j) s_ij,
 //       A1 = sum_ij ex(i) (i + 1/2 - x) ey(j) s_ij, A2 likewise with
 //       (j + 1/2 - y), by column chunks of 16: R_i = sum_j ey(j) s_ij,
 //       C_j += ex(i) s_ij (s rows read as LDS broadcasts), the lane's own
-//       factors by recurrence in registers.  Two FMAs per pixel-star and no
-//       cross-lane reduction.
+//       factors by recurrence in registers.  Two FMAs per pixel-star; a star's
+//       rows are split over G = 1, 2 or 4 lanes (dense_log2_groups: few stars
+//       would leave most lanes idle) whose partial sums one or two quad DPP
+//       adds combine.
 //   dVdq = (-A0, -A1 f / var, -A2 f / var) (:404-406).
 //
 // Nothing is truncated (full image, any PSF width).
@@ -60,6 +62,22 @@ __device__ __forceinline__ void gauss_run8(double v0, double scale, const double
   }
 }
 
+// Row groups per star in the dense kernel's pass 3 (log2): the G in {1, 2, 4}
+// with the fewest row-units ceil(G K / 64) / G per lane, the smallest on a
+// tie — K <= 16: 4 (a quarter of the rows per lane), K <= 32: 2, K = 100: 4
+// (7 rounds of a quarter against 2 full rounds).
+__host__ __device__ __forceinline__ int dense_log2_groups(int K) {
+  int best = 0, best_cost = 4 * ((K + 63) / 64);
+  for (int lg = 1; lg <= 2; ++lg) {
+    const int cost = (4 >> lg) * (((K << lg) + 63) / 64);
+    if (cost < best_cost) {
+      best = lg;
+      best_cost = cost;
+    }
+  }
+  return best;
+}
+
 template <int IMG>
 struct DenseG {
   static_assert(IMG == 32 || IMG == 48, "image side");
@@ -67,9 +85,16 @@ struct DenseG {
   static constexpr int TK = 16;         // stars per factor-table tile (divides 64)
   static constexpr int CW = 16;         // pass-3 column chunk
   static constexpr int NCH = IMG / CW;
-  // per wave: the tile tables ex [TK][IMG] + fey [TK][IMG], later s [IMG][IMG]
+  // LDS bank spreading (64 banks of 4 bytes): the tile tables' rows are TP
+  // doubles apart (a 16-byte multiple whose 16 rows start in 16 different bank
+  // quads: 32 px 68 dwords = 4 mod 64, 48 px 100 = 36 mod 64), so the table
+  // builder's stores (one row per lane) do not conflict; s is [IMG][IMG] with
+  // the rows of pass-3 row group g shifted by 2 g doubles (16 g bytes), so
+  // the G groups' simultaneous row reads hit different banks.
+  static constexpr int TP = IMG + 2;
+  // per wave: the tile tables ex [TK][TP] + fey [TK][TP], later s (+ skews)
   static __host__ __device__ constexpr size_t wave_doubles() {
-    return 2 * TK * IMG > IMG * IMG ? (size_t)2 * TK * IMG : (size_t)IMG * IMG;
+    return 2 * TK * TP > IMG * IMG + 8 ? (size_t)2 * TK * TP : (size_t)IMG * IMG + 8;
   }
   // LDS: exp table, the image (fp64, [IMG][IMG]), the waves' regions
   static __host__ __device__ constexpr size_t lds_bytes(int waves) {
@@ -116,8 +141,8 @@ struct DenseG {
     const int a = lane >> 3, b = lane & 7;
 #pragma unroll
     for (int u = 0; u < BS * BS; ++u) lam[u] = c.B;
-    double* ext = g.w;               // [TK][IMG]
-    double* fyt = g.w + TK * IMG;    // [TK][IMG]
+    double* ext = g.w;              // [TK][TP]
+    double* fyt = g.w + TK * TP;    // [TK][TP]
     // table builder: lane -> (row rr = lane / 2: star rr % 16, axis rr / 16;
     // half h = lane % 2 of the entries)
     const int rr = lane >> 1, h = lane & 1;
@@ -131,7 +156,7 @@ struct DenseG {
       const double fs = __shfl(pick<SLOTS>(f, s), src, kWave);
       const double ctr = axis ? ys : xs;
       const double scale = axis ? fs * lc.inv_norm : 1.0;
-      double* dst = (axis ? fyt : ext) + rs * IMG + h * HALF;
+      double* dst = (axis ? fyt : ext) + rs * TP + h * HALF;
       wave_lds_sync();  // the previous tile's reads are done
 #pragma unroll
       for (int r0 = 0; r0 < HALF; r0 += 8) {
@@ -145,9 +170,9 @@ struct DenseG {
       for (int r = 0; r < nk; ++r) {  // stars in ascending order
         double ex[BS], fy[BS];
 #pragma unroll
-        for (int u = 0; u < BS; ++u) ex[u] = ext[r * IMG + a * BS + u];
+        for (int u = 0; u < BS; ++u) ex[u] = ext[r * TP + a * BS + u];
 #pragma unroll
-        for (int v = 0; v < BS; ++v) fy[v] = fyt[r * IMG + b * BS + v];
+        for (int v = 0; v < BS; ++v) fy[v] = fyt[r * TP + b * BS + v];
 #pragma unroll
         for (int u = 0; u < BS; ++u)
 #pragma unroll
@@ -166,6 +191,8 @@ struct DenseG {
                                                   const LeanConsts& lc, bool with_metric,
                                                   double (&gf)[SLOTS], double (&gx)[SLOTS],
                                                   double (&gy)[SLOTS]) {
+    const int lgG = dense_log2_groups(K);
+    const int rows = IMG >> lgG;
     {
       const int lane = lane_id();
       double lam[BS * BS];
@@ -174,8 +201,9 @@ struct DenseG {
       const int a = lane >> 3, b = lane & 7;
 #pragma unroll
       for (int u = 0; u < BS; ++u) {
-        const double* drow = g.img + (a * BS + u) * IMG + b * BS;
-        double* srow = g.w + (a * BS + u) * IMG + b * BS;
+        const int i = a * BS + u;
+        const double* drow = g.img + i * IMG + b * BS;
+        double* srow = g.w + i * IMG + 2 * (i / rows) + b * BS;
 #pragma unroll
         for (int v = 0; v < BS; v += 2) {
           const double l0 = lam[u * BS + v], l1 = lam[u * BS + v + 1];
@@ -186,12 +214,23 @@ struct DenseG {
       }
     }
     wave_lds_sync();
-    // pass 3: lane = star
+    // pass 3: work item t = 64 r + lane of round r is (star t / G, row group
+    // t % G); the G lanes of a star sum their partial A0, A1, A2 (quad DPP)
+    // and the star's owner lane (64 s + l in slot s) reads them.
+    const int lane = lane_id();
+    const int G = 1 << lgG;
+    const int rounds = (K * G + kWave - 1) / kWave;
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s) {
-      gf[s] = gx[s] = gy[s] = 0.0;
-      if (kWave * s >= K) continue;  // wave-uniform
-      const double xs = x[s], ys = y[s];
+    for (int s = 0; s < SLOTS; ++s) gf[s] = gx[s] = gy[s] = 0.0;
+    for (int r = 0; r < rounds; ++r) {  // wave-uniform
+      const int k0 = (kWave * r) >> lgG;             // the round's first star
+      const int ks = k0 / kWave;                      // its slot (64 / G divides 64)
+      const int t = kWave * r + lane;
+      const int src = (t >> lgG) & (kWave - 1);
+      const int ib = (t & (G - 1)) * rows;            // the item's first row
+      const double* sbase = g.w + 2 * (t & (G - 1));  // the row group's skew
+      const double xs = __shfl(pick<SLOTS>(x, ks), src, kWave);
+      const double ys = __shfl(pick<SLOTS>(y, ks), src, kWave);
       double A0 = 0.0, A1 = 0.0, A2 = 0.0;
 #pragma unroll 1
       for (int ch = 0; ch < NCH; ++ch) {
@@ -209,12 +248,14 @@ struct DenseG {
 #pragma unroll
         for (int j = 0; j < CW; ++j) C[j] = 0.0;
 #pragma unroll 1
-        for (int i0 = 0; i0 < IMG; i0 += 8) {
+        for (int di = 0; di < rows; di += 8) {       // rows: wave-uniform
+          const int i0 = ib + di;
           double ex[8];
           gauss_run8(((double)i0 + 0.5) - xs, 1.0, g.etab, lc, ex);
 #pragma unroll
           for (int l = 0; l < 8; ++l) {
-            const double* sr = g.w + (i0 + l) * IMG + j0;  // broadcast reads
+            if (di + l >= rows) break;                 // wave-uniform (48 px, G = 4)
+            const double* sr = sbase + (i0 + l) * IMG + j0;  // G distinct rows: broadcasts
             double r0 = 0.0, r1 = 0.0;
 #pragma unroll
             for (int j = 0; j < CW; j += 2) {
@@ -233,9 +274,30 @@ struct DenseG {
 #pragma unroll
         for (int j = 0; j < CW; ++j) A2 = fma(ey[j] * (((double)(j0 + j) - ys) + 0.5), C[j], A2);
       }
-      gf[s] = -A0;                        // :404
-      gx[s] = -A1 * f[s] * lc.inv_var;    // :405
-      gy[s] = -A2 * f[s] * lc.inv_var;    // :406
+      if (lgG >= 1) {  // sum over the star's G lanes (every lane gets the same bits)
+        A0 += dpp_move<0xB1>(A0);
+        A1 += dpp_move<0xB1>(A1);
+        A2 += dpp_move<0xB1>(A2);
+      }
+      if (lgG >= 2) {
+        A0 += dpp_move<0x4E>(A0);
+        A1 += dpp_move<0x4E>(A1);
+        A2 += dpp_move<0x4E>(A2);
+      }
+      // owner lanes of the round's stars: k0 % 64 <= lane < k0 % 64 + 64 / G
+      const int rel = lane - (k0 & (kWave - 1));
+      const bool mine = rel >= 0 && rel < (kWave >> lgG) && k0 + rel < K;
+      const int from = mine ? rel << lgG : lane;
+      const double a0 = __shfl(A0, from, kWave), a1 = __shfl(A1, from, kWave),
+                   a2 = __shfl(A2, from, kWave);
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        if (s == ks && mine) {
+          gf[s] = -a0;                        // :404
+          gx[s] = -a1 * f[s] * lc.inv_var;    // :405
+          gy[s] = -a2 * f[s] * lc.inv_var;    // :406
+        }
+      }
     }
     wave_lds_sync();  // s is read; the next gradient's tables may overwrite it
 #pragma unroll

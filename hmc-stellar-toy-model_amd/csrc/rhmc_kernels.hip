@@ -1108,13 +1108,13 @@ void pick_waves_path(const rhmc_ctx* ctx, int path, int K, size_t* lds, int* W) 
 // covers most of the image); RHMC_KERNEL_DENSE forces it on those images at
 // any K, GENERIC / WINDOWED keep the per-wave families, MULTIWIN(_NOTAB)
 // keeps the multi-star register-window kernel where it applies (K <= 64).
-// Measured against the multi-star register-window kernel (4096 chains, 100
-// steps, chain-steps/s, profiles/r04_dense/): 32 px K = 12 6.7e7 vs 7.5e7,
-// K = 16 6.6e7 vs 5.0e7, K = 24 5.6e7 vs 1.6e7; 48 px K = 12 2.6e7 vs 4.5e7,
-// K = 16 2.6e7 vs 2.6e7, K = 24 2.4e7 vs 1.6e7, K = 40 2.2e7 vs 6.3e6;
-// big-sim4 (32 px, K = 51) 4.2e7 vs 3.7e6, big-sim3 (K = 100) 2.2e7 vs 1.7e5
-// for the windowed kernel.
-constexpr int kDenseMinK = 16;
+// Measured (4096 chains, 100 steps, chain-steps/s, profiles/r04_dense/):
+// against the multi-star register-window kernel 32 px K = 12 1.15e8 vs 7.4e7,
+// K = 24 8.1e7 vs 1.6e7; 48 px K = 12 5.6e7 vs 4.5e7, K = 24 3.6e7 vs 1.6e7,
+// K = 40 2.3e7 vs 6.4e6; big-sim4 (32 px, K = 51) 5.1e7 vs 3.8e6, big-sim3
+// (K = 100) 2.7e7 vs 1.7e5 for the windowed kernel.  At K <= 10 the
+// pixel-major kernel stays (48 px K = 10: 2.2e8 vs 4.2e7).
+constexpr int kDenseMinK = 11;
 bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c);
 int dense_path(const rhmc_ctx* ctx, int K, const Consts& c) {
   if (ctx->rows != ctx->cols || (ctx->rows != 32 && ctx->rows != 48)) return 0;
