@@ -324,6 +324,9 @@ def main():
                          "datagen: --n-real Poisson realisations of the workload's model "
                          "image (rhmc_gen_image)")
     ap.add_argument("--mh-iter", type=int, default=10)
+    ap.add_argument("--f-pos", type=int, choices=(0, 1), default=1,
+                    help="--mode mh: run_RHMC's f_pos (V = inf below the flux wall, "
+                         "sampler_RHMC.py:303-309; the reference's default 1)")
     ap.add_argument("--mh-unfused", action="store_true",
                     help="--mode mh: the four-kernel loop (RHMC_OPT_MH_FUSED = 0)")
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
@@ -409,8 +412,8 @@ def main():
             ctx.set_option(capi.OPT_MH_FUSED, 0)
 
         def launch():
-            ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap, f_pos=True,
-                          seed=1234 + rank, stream=stream.cuda_stream)
+            ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap,
+                          f_pos=bool(args.f_pos), seed=1234 + rank, stream=stream.cuda_stream)
     elif args.mode == "integrate":
         solver = {"hmc": capi.SOLVER_HMC, "naive": capi.SOLVER_RHMC_NAIVE,
                   "leap_frog": capi.SOLVER_RHMC_LEAPFROG}[args.solver]
@@ -508,6 +511,7 @@ def main():
                    "image": list(wl.D.shape), "K": wl.K,
                    "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
                    "mh_fused": (None if args.mode != "mh" else not args.mh_unfused),
+                   "f_pos": (None if args.mode != "mh" else args.f_pos),
                    "solver": (args.solver if args.mode == "integrate" else
                               "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},

@@ -37,30 +37,7 @@
 
 namespace rhmc {
 
-// e[l] = exp(-c (v0 + l)^2), l < 8: by recurrence from two exps when v0 is
-// within the recurrence's range (e(v + 1) = e(v) g(v), g(v + 1) = g(v) e^-2c,
-// g(v) = exp(-c (2 v + 1)); Consts::rec_vmax), else eight direct exps (a far
-// or NaN star: a per-lane branch).  Scaled by `scale`.
-__device__ __forceinline__ void gauss_run8(double v0, double scale, const double* __restrict__ etab,
-                                           const LeanConsts& lc, double (&e)[8]) {
-  const double c = lc.inv_two_sig2;
-  if (fabs(v0) < lc.rec_vmax) {
-    double ev = exp_neg(-(v0 * v0) * c, etab) * scale;
-    double g = exp_neg(-fma(2.0, v0, 1.0) * c, etab);
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      e[l] = ev;
-      ev = ev * g;
-      g = g * lc.k_row;
-    }
-  } else {
-#pragma unroll
-    for (int l = 0; l < 8; ++l) {
-      const double v = v0 + (double)l;
-      e[l] = exp_neg(-(v * v) * c, etab) * scale;
-    }
-  }
-}
+// gauss_run8: rhmc_windowed.hpp.
 
 // Row groups per star in the dense kernel's pass 3 (log2): the G in {1, 2, 4}
 // with the fewest row-units ceil(G K / 64) / G per lane, the smallest on a

@@ -1084,11 +1084,10 @@ bool use_windowed(const rhmc_ctx* ctx, int K) {
 
 // Windowed kernels: W waves per workgroup, LDS = W * tables.
 void pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
-  const size_t per = win_table_doubles(K) * sizeof(double);
   int w = 4;
-  while (w > 1 && w * per > (size_t)ctx->max_lds) w >>= 1;
+  while (w > 1 && WinG::lds_bytes(w, K) > (size_t)ctx->max_lds) w >>= 1;
   *W = w;
-  *lds = w * per;  // K <= 256: 135 KB for one wave, within the CU's 160 KB
+  *lds = WinG::lds_bytes(w, K);  // K <= 256: 136 KB for one wave, within the CU's 160 KB
 }
 
 // The slotted kernels' workgroup for a path (with_path): the windowed tables'
@@ -1403,10 +1402,15 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   const int path = dense_path(ctx, K, c);
   const bool win = path || use_windowed(ctx, K);
   if (win && !path && !window_exact(c)) return window_unsupported();
-  if (win)
+  if (win && !path) {  // potential-only windowed tables (WinEG)
+    W = 4;
+    while (W > 1 && WinEG::lds_bytes(W, K) > (size_t)ctx->max_lds) W >>= 1;
+    lds = WinEG::lds_bytes(W, K);
+  } else if (win) {
     pick_waves_path(ctx, path, K, &lds, &W);
-  else if ((rc = pick_waves(ctx, K, &lds, &W)))
+  } else if ((rc = pick_waves(ctx, K, &lds, &W))) {
     return rc;
+  }
   a.q = d_q;
   a.p = d_p;
   a.V = d_V;
@@ -1418,12 +1422,13 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.g = make_geometry(ctx->rows, ctx->cols);
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
-    return with_path(path, K, [&](auto gt, auto st) {
+    auto go = [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
       hipLaunchKernelGGL((energy_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a);
       HIP_TRY(hipGetLastError());
       return (int)RHMC_OK;
-    });
+    };
+    return path ? with_path(path, K, go) : with_slots<WinEG>(K, go);
   }
   return dispatch_k<EnergyLaunch>(K, grid, block, lds, s, a);
 }
@@ -1857,7 +1862,10 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
   // V reads beta through the repulsion term: a beta schedule re-evaluates
   // V(q) at each iteration's start, like the reference's V_initial (:1025)
   const bool v_sched = sched && c.use_Vc && sc->beta && sc->n_beta > 0;
-  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  // begin / end: one thread per chain for few stars, one wave per chain
+  // (lanes over the coordinates) from 8 stars
+  const bool wave_mh = K >= 8;
+  const dim3 grid((unsigned)(wave_mh ? (n + 3) / 4 : (n + 255) / 256)), block(256);
   for (int it = 0; it < n_iter; ++it) {
     m.iter = it;
     const rhmc_params Pl = sched ? sched_params(*P, sc, it) : *P;
@@ -1867,13 +1875,19 @@ int run_mh(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, int64_t n, int32_t 
           (rc = launch_energy(ctx, m.c, d_q, nullptr, m.V_cur, nullptr, n, K, f_pos, s)))
         return rc;
     }
-    hipLaunchKernelGGL(mh_begin_kernel, grid, block, 0, s, m);
+    if (wave_mh)
+      hipLaunchKernelGGL(mh_begin_wave_kernel, grid, block, 0, s, m);
+    else
+      hipLaunchKernelGGL(mh_begin_kernel, grid, block, 0, s, m);
     HIP_TRY(hipGetLastError());
     if ((rc = launch_leapfrog(ctx, &Pl, m.q_prop, m.p, n, K, n_steps, nullptr, nullptr, s)))
       return rc;
     if ((rc = launch_energy(ctx, m.c, m.q_prop, nullptr, m.V_prop, nullptr, n, K, f_pos, s)))
       return rc;
-    hipLaunchKernelGGL(mh_end_kernel, grid, block, 0, s, m);
+    if (wave_mh)
+      hipLaunchKernelGGL(mh_end_wave_kernel, grid, block, 0, s, m);
+    else
+      hipLaunchKernelGGL(mh_end_kernel, grid, block, 0, s, m);
     HIP_TRY(hipGetLastError());
   }
   return RHMC_OK;

@@ -163,4 +163,72 @@ __global__ void __launch_bounds__(256) mh_end_kernel(MhArgs a) {
   if (a.accept) a.accept[(int64_t)a.iter * a.n + ch] = acc ? 1 : 0;
 }
 
+// The same two steps with one wave per chain, lanes over the 3K coordinates
+// (many stars: one thread per chain would leave most of the GPU idle, e.g.
+// 4096 chains of K = 51 = 64 busy SIMDs).  T's two sums are wave sums
+// (numpy's np.sum is pairwise: no order is the reference's exactly).
+__global__ void __launch_bounds__(256) mh_begin_wave_kernel(MhArgs a) {
+  const int64_t ch = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (ch >= a.n) return;
+  const int lane = lane_id();
+  const int d = 3 * a.K;
+  const double* q = a.q + ch * d;
+  double* p = a.p + ch * d;
+  double* qp = a.q_prop + ch * d;
+  const int64_t r = (int64_t)a.iter * a.n + ch;
+  double t1 = 0.0, t2 = 0.0;
+  for (int idx = lane; idx < d; idx += kWave) {
+    double hff, hxx;
+    metric_pair(q[idx - idx % 3], a.c, hff, hxx);
+    const double h = (idx % 3 == 0) ? hff : hxx;
+    const double zz = a.z ? a.z[((int64_t)a.iter * a.n + ch) * d + idx]
+                          : philox_normal(a.seed, ch, a.iter, idx);
+    const double pv = zz * sqrt(h);                 // u_sample(d) * np.sqrt(H_diag) (:1022)
+    p[idx] = pv;
+    qp[idx] = q[idx];
+    if (a.q_chain) a.q_chain[r * d + idx] = q[idx];
+    t1 += pv * pv / h;
+    t2 += log(fabs(h));
+  }
+  const double T0 = (wave_sum(t1) + wave_sum(t2)) / 2.0;  // (:353-363)
+  if (lane == 0) {
+    const double V0 = a.V_cur[ch];
+    const double E0 = V0 + T0;
+    a.E0[ch] = E0;
+    if (a.V_chain) a.V_chain[r] = V0;
+    if (a.T_chain) a.T_chain[r] = T0;
+    if (a.E_chain) a.E_chain[r] = E0;
+  }
+}
+
+__global__ void __launch_bounds__(256) mh_end_wave_kernel(MhArgs a) {
+  const int64_t ch = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+  if (ch >= a.n) return;
+  const int lane = lane_id();
+  const int d = 3 * a.K;
+  const double* qp = a.q_prop + ch * d;
+  const double* p = a.p + ch * d;
+  double t1 = 0.0, t2 = 0.0;
+  for (int idx = lane; idx < d; idx += kWave) {
+    double hff, hxx;
+    metric_pair(qp[idx - idx % 3], a.c, hff, hxx);
+    const double h = (idx % 3 == 0) ? hff : hxx;
+    t1 += p[idx] * p[idx] / h;
+    t2 += log(fabs(h));
+  }
+  const double V1 = a.V_prop[ch];
+  const double E1 = V1 + (wave_sum(t1) + wave_sum(t2)) / 2.0;
+  const double dE = E1 - a.E0[ch];
+  const double uu = a.u ? a.u[(int64_t)a.iter * a.n + ch] : philox_uniform(a.seed, ch, a.iter);
+  const bool acc = (dE < 0.0) || (log(uu) < -dE);   // :1076 (wave-uniform)
+  if (acc) {
+    double* q = a.q + ch * d;
+    for (int idx = lane; idx < d; idx += kWave) q[idx] = qp[idx];
+  }
+  if (lane == 0) {
+    if (acc) a.V_cur[ch] = V1;
+    if (a.accept) a.accept[(int64_t)a.iter * a.n + ch] = acc ? 1 : 0;
+  }
+}
+
 }  // namespace rhmc

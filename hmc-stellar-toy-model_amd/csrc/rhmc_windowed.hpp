@@ -23,6 +23,7 @@
 // D stays in global memory (512 KB at 256x256, L2-resident and shared by all
 // chains).  Per-wave LDS: windowed PSF factor tables, 2 x K x 33 doubles.
 #pragma once
+#include "rhmc_exp.hpp"
 #include "rhmc_wave.hpp"
 
 namespace rhmc {
@@ -232,14 +233,83 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
   wave_lds_sync();
 }
 
-// V of the wave's chain on a large image (sampler_RHMC.py:294-351), pixel-major:
-// image row i (uniform), lanes over columns; only the stars whose window rows
-// contain i contribute (one ballot per slot).
+// Column factor tables only (the potential's; the row factors are per-row
+// scalars there): ey [K][kTabW], flattened over (star, index) like
+// win_build_tables.
 template <int SLOTS>
-__device__ double win_potential(const double* __restrict__ D, const WinTables& t, int K,
+__device__ __forceinline__ void win_build_ey(double* ey, int K, const double (&y)[SLOTS],
+                                             const int (&by)[SLOTS], const LeanConsts& lc) {
+  const int lane = lane_id();
+#pragma unroll
+  for (int s = 0; s < SLOTS; ++s) {
+    const int k0 = kWave * s;
+    if (k0 >= K) break;  // wave-uniform
+    const int Ks = min(kWave, K - k0);
+    const int total = Ks * kTabW;
+    const int iters = (total + kWave - 1) / kWave;
+    for (int m = 0; m < iters; ++m) {  // uniform trip count: shuffles see all lanes
+      const int e = lane + kWave * m;
+      const int kl = min(e / kTabW, Ks - 1);
+      const double yk = __shfl(y[s], kl, kWave);
+      const int byk = __shfl(by[s], kl, kWave);
+      if (e < total) {
+        const int d = e - kl * kTabW;
+        double val = 0.0;
+        if (d < kWin) {
+          const double v = ((double)(byk + d) + 0.5) - yk;
+          val = exp(-(v * v) * lc.inv_two_sig2) * lc.inv_norm;
+        }
+        ey[(k0 + kl) * kTabW + d] = val;
+      }
+    }
+  }
+  wave_lds_sync();
+}
+
+// e[l] = exp(-c (v0 + l)^2), l < 8: by recurrence from two exps when v0 is
+// within the recurrence's range (e(v + 1) = e(v) g(v), g(v + 1) = g(v) e^-2c,
+// g(v) = exp(-c (2 v + 1)); Consts::rec_vmax), else eight direct exps (a far
+// or NaN star: a per-lane branch).  Scaled by `scale`.
+__device__ __forceinline__ void gauss_run8(double v0, double scale, const double* __restrict__ etab,
+                                           const LeanConsts& lc, double (&e)[8]) {
+  const double c = lc.inv_two_sig2;
+  if (fabs(v0) < lc.rec_vmax) {
+    double ev = exp_neg(-(v0 * v0) * c, etab) * scale;
+    double g = exp_neg(-fma(2.0, v0, 1.0) * c, etab);
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      e[l] = ev;
+      ev = ev * g;
+      g = g * lc.k_row;
+    }
+  } else {
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+      const double v = v0 + (double)l;
+      e[l] = exp_neg(-(v * v) * c, etab) * scale;
+    }
+  }
+}
+
+// V of the wave's chain on a large image (sampler_RHMC.py:294-351), pixel-major
+// in groups of kPotRows image rows (uniform) with lanes over columns in blocks
+// of 64.  Only the stars whose window rows meet the group and whose window
+// columns reach the block contribute (one ballot per slot for each): one
+// column-factor load from the ey table per (star, block) serves all rows of
+// the group, the row factors f ex(i) being per-row scalars of the star's lane
+// (gauss_run8's recurrence from two table exps, zero outside its window
+// rows).  A block no star reaches has Lambda == B exactly (the window bound)
+// and adds B - D ln B per pixel without a log.  ln by log_pos (rhmc_exp.hpp:
+// within 2 ulp, ~25 VALU).
+constexpr int kPotRows = 8;  // a multiple of 8 (gauss_run8)
+
+template <int SLOTS>
+__device__ double win_potential(const double* __restrict__ D, double* ey,
+                                const double* __restrict__ etab, int K,
                                 const double (&f)[SLOTS], const double (&x)[SLOTS],
                                 const double (&y)[SLOTS], int rows, int cols, const Consts& c,
                                 const LeanConsts& lc) {
+  constexpr int R = kPotRows;
   const int lane = lane_id();
   int bx[SLOTS], by[SLOTS];
 #pragma unroll
@@ -247,32 +317,80 @@ __device__ double win_potential(const double* __restrict__ D, const WinTables& t
     bx[s] = win_base(x[s]);
     by[s] = win_base(y[s]);
   }
-  win_build_tables<SLOTS>(t, K, x, y, bx, by, lc);
+  win_build_ey<SLOTS>(ey, K, y, by, lc);
+  const double lnB = log_pos(c.B);
   double v = 0.0;
-  for (int i = 0; i < rows; ++i) {
+  for (int i0 = 0; i0 < rows; i0 += R) {
     unsigned long long rm[SLOTS];
+    double fex[SLOTS][R];
+    bool any_row = false;
 #pragma unroll
-    for (int s = 0; s < SLOTS; ++s)
-      rm[s] = __builtin_amdgcn_ballot_w64(win_own(s, K) && bx[s] <= i && i < bx[s] + kWin);
-    for (int cb = 0; cb < cols; cb += kWave) {
-      const int j = cb + lane;
-      if (j < cols) {
-        double lam = c.B;
+    for (int s = 0; s < SLOTS; ++s) {
+      const bool meet = win_own(s, K) && bx[s] < i0 + R && i0 < bx[s] + kWin;
+      rm[s] = __builtin_amdgcn_ballot_w64(meet);
+      any_row = any_row || rm[s] != 0ull;
 #pragma unroll
-        for (int s = 0; s < SLOTS; ++s) {
-          unsigned long long mm = rm[s];
-          while (mm) {
-            const int kl = __builtin_ctzll(mm);
-            mm &= mm - 1;
-            const int kk = kWave * s + kl;
-            const double fkk = bcast(f[s], kl);
-            const int u = i - readlane_i(bx[s], kl);
-            const unsigned vv = min((unsigned)(j - readlane_i(by[s], kl)), (unsigned)kWin);
-            lam = fma(fkk, t.ex[kk * kTabW + u] * t.ey[kk * kTabW + vv], lam);
+      for (int r = 0; r < R; ++r) fex[s][r] = 0.0;
+      if (meet) {  // per lane: the star's f ex(i) on the group's window rows
+#pragma unroll
+        for (int h = 0; h < R; h += 8) {
+          double e[8];
+          gauss_run8(((double)(i0 + h) + 0.5) - x[s], f[s], etab, lc, e);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) {
+            const int i = i0 + h + r;
+            fex[s][h + r] = (bx[s] <= i && i < bx[s] + kWin) ? e[r] : 0.0;
           }
         }
-        v += lam - D[(size_t)i * cols + j] * log(lam);
       }
+    }
+    const int nr = min(R, rows - i0);
+    for (int cb = 0; cb < cols; cb += kWave) {
+      const int j = cb + lane;
+      const bool jin = j < cols;
+      unsigned long long bm[SLOTS];
+      bool any = false;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        bm[s] = any_row ? rm[s] & __builtin_amdgcn_ballot_w64(by[s] < cb + kWave &&
+                                                                by[s] + kWin > cb)
+                        : 0ull;
+        any = any || bm[s] != 0ull;
+      }
+      double d[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        d[r] = (jin && r < nr) ? D[(size_t)(i0 + r) * cols + j] : 0.0;
+      if (!any) {  // wave-uniform: Lambda == B on the whole block
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+          if (jin && r < nr) v += c.B - d[r] * lnB;
+        continue;
+      }
+      double lam[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) lam[r] = c.B;
+#pragma unroll
+      for (int s = 0; s < SLOTS; ++s) {
+        unsigned long long mm = bm[s];
+        while (mm) {
+          const int kl = __builtin_ctzll(mm);
+          mm &= mm - 1;
+          const int kk = kWave * s + kl;
+          const unsigned vv = min((unsigned)(j - readlane_i(by[s], kl)), (unsigned)kWin);
+          const double e = ey[kk * kTabW + vv];
+#pragma unroll
+          for (int r = 0; r < R; ++r) lam[r] = fma(bcast(fex[s][r], kl), e, lam[r]);
+        }
+      }
+      // The R rows' logs unconditionally (lam is finite on masked rows), so
+      // their independent chains interleave; masked terms dropped by select.
+      double lg[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) lg[r] = log_pos(lam[r]);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+        v += (jin && r < nr) ? lam[r] - d[r] * lg[r] : 0.0;
     }
   }
   wave_lds_sync();
@@ -283,17 +401,21 @@ __device__ double win_potential(const double* __restrict__ D, const WinTables& t
 // tables: any square image, D read from global memory (L2).
 struct WinG {
   static __host__ __device__ size_t lds_bytes(int waves, int K) {
-    return (size_t)waves * win_table_doubles(K) * sizeof(double);
+    return (kExpTab + (size_t)waves * win_table_doubles(K)) * sizeof(double);
   }
   struct Ctx {
     WinTables tab;
+    const double* etab;
     const double* D;
     int rows, cols;
   };
   static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
                                               int cols) {
-    double* base = lds + (threadIdx.x / kWave) * win_table_doubles(K);
+    exp_tab_fill(lds);
+    __syncthreads();
+    double* base = lds + kExpTab + (threadIdx.x / kWave) * win_table_doubles(K);
     Ctx g;
+    g.etab = lds;
     g.tab = WinTables{base, base + K * kTabW};
     g.D = D;
     g.rows = rows;
@@ -315,7 +437,42 @@ struct WinG {
                                                      const double (&x)[SLOTS],
                                                      const double (&y)[SLOTS], const Consts& c,
                                                      const LeanConsts& lc) {
-    return win_potential<SLOTS>(g.D, g.tab, K, f, x, y, g.rows, g.cols, c, lc);
+    return win_potential<SLOTS>(g.D, g.tab.ex, g.etab, K, f, x, y, g.rows, g.cols, c, lc);
+  }
+};
+
+// The potential-only policy of the energy kernel on windowed tables: the
+// column tables alone (K x 33 doubles per wave, half WinG's), so twice the
+// waves fit a CU (C5: 2 per SIMD instead of 1).
+struct WinEG {
+  static __host__ __device__ size_t lds_bytes(int waves, int K) {
+    return (kExpTab + (size_t)waves * K * kTabW) * sizeof(double);
+  }
+  struct Ctx {
+    double* ey;
+    const double* etab;
+    const double* D;
+    int rows, cols;
+  };
+  static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
+                                              int cols) {
+    exp_tab_fill(lds);
+    __syncthreads();
+    Ctx g;
+    g.etab = lds;
+    g.ey = lds + kExpTab + (threadIdx.x / kWave) * (size_t)K * kTabW;
+    g.D = D;
+    g.rows = rows;
+    g.cols = cols;
+    return g;
+  }
+  template <int SLOTS>
+  static __device__ __forceinline__ double potential(const Ctx& g, int K,
+                                                     const double (&f)[SLOTS],
+                                                     const double (&x)[SLOTS],
+                                                     const double (&y)[SLOTS], const Consts& c,
+                                                     const LeanConsts& lc) {
+    return win_potential<SLOTS>(g.D, g.ey, g.etab, K, f, x, y, g.rows, g.cols, c, lc);
   }
 };
 

@@ -9,7 +9,9 @@ C5  256x256, K = 64, 8,192 chains, prior on (leapfrog_kr<float, 2, false>).
 Checked: an oracle sample with exact fixed-point iteration counts (C3: 4
 chains x the first 100 steps — the chaotic horizon of the reference itself at
 C3 is ~100-130 steps, so the sample uses chains whose 1e-15 perturbation stays
-below 1e-11 for 100 steps, measured with the oracle; C5: 2 chains x 5 steps);
+below 1e-11 for 100 steps, measured with the oracle; C5: 4 chains x 20 steps,
+through the flux wall; tests/golden/traj_c5.npz pins C5 to the reference
+itself, 4 chains x 50 steps, in tests/test_gpu_parity.py);
 batch invariance (ragged subsets spanning waves give bit-identical results);
 determinism; launch segmentation (5 x 100 == 1 x 500 bit for bit); and the
 near-wall reflection fraction SURVEY §8(c) asks to report separately.
@@ -102,13 +104,18 @@ def test_c3_launch_segmentation(c3):
 
 
 def test_c5_full_size_oracle_sample(c5):
+    """4 chains x 20 steps of the 8192-chain C5 launch against the oracle;
+    the flux wall (sampler_RHMC.py:554-559) fires in the sample (the prior,
+    :408-409, is on)."""
     capi, wl, ctx, P, (q, p, it, st) = c5
     assert q.shape == (8192, 192)
     assert not (st & capi.STATUS_NONFINITE).any()
     near = (st & capi.STATUS_NEAR_WALL) != 0
     print("C5 500 steps: %d chains within 2^-40 of a wall (%.2e)" % (near.sum(), near.mean()))
     assert near.mean() < 1e-2
-    _oracle_sample(capi, wl, ctx, P, (0, 8191), 5)
+    sample = (0, 2731, 5462, 8191)
+    st20 = _oracle_sample(capi, wl, ctx, P, sample, 20)
+    assert any(st20[c] & capi.STATUS_REFLECT_F for c in sample)
 
 
 def test_c5_batch_invariance_determinism_segmentation(c5):
