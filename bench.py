@@ -519,6 +519,9 @@ def main():
         "nonfinite_chains": nonfinite,
         "fixed_point_iters_per_step": fp_stats,
         "per_rank": per_rank,
+        # the kernel sources this line ran (sha256/16 of csrc/*, Makefile, rhmc.h:
+        # the same hash pmc_summary.py stores; the GPU box has no .git)
+        "sources": source_hash(),
     }
     if args.mode == "leapfrog" and not args.no_e2e and world == 1:
         out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)

@@ -655,6 +655,138 @@ class multi_gym(base_class):
         self.A_chain = out["accept"].astype(bool)
         return out["q"]
 
+    def run_RHMC_rj_batched(self, q_models_0, seeds, f_pos=True, delta=1e-6, Niter=100,
+                            Nsteps=100, dt=1e-1, counter_max=1000, N_max=50,
+                            P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None):
+        """Many independent chains of run_RHMC WITH the reversible-jump moves
+        (sampler_RHMC.py:937-1198; birth_death_move :1200-1270, split_merge_move
+        :1273-1445), each chain at its own, changing, star count.  Chain c is
+        run_RHMC after np.random.seed(seeds[c]): its draws come from its own
+        NumPy stream in the reference's order (swapped into the global stream
+        around its host work, so the moves' np.random / scipy Beta draws are
+        the reference's own), while the GPU work of every phase — V(q) at the
+        iteration start, the Nsteps trajectories before and after a jump, V(q')
+        — runs batched over the chains, one launch per distinct star count
+        (chains grouped by K, so the kernels see ordinary fixed-K batches).
+
+        q_models_0: a list of [K_c, 3] (mag, x, y) arrays.  Returns a list of
+        the chains' final q; sets q_chain / p_chain [Niter+1, n, 3 N_max],
+        E/V/T_chain, A_chain, move_chain, N_chain [Niter+1, n] (iteration-major,
+        like run_RHMC_batched)."""
+        n = len(q_models_0)
+        if len(seeds) != n:
+            raise ValueError("one seed per chain")
+        self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
+        self.P_move, self.N_max = P_move, N_max
+        n_it = Niter + 1
+        self.q_chain = np.zeros((n_it, n, N_max * 3))
+        self.p_chain = np.zeros((n_it, n, N_max * 3))
+        self.E_chain, self.V_chain, self.T_chain = (np.zeros((n_it, n)) for _ in range(3))
+        self.A_chain = np.zeros((n_it, n), dtype=bool)
+        self.move_chain = np.zeros((n_it, n), dtype=int)
+        self.N_chain = np.zeros((n_it, n), dtype=int)
+        saved = np.random.get_state()
+        states = []
+        for s in seeds:
+            np.random.seed(s)
+            states.append(np.random.get_state())
+        q = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
+        p = [None] * n
+        move = [0] * n
+        grow = [False] * n
+        E0 = np.zeros(n)
+        factor = np.zeros(n)
+
+        def host(c, fn):               # chain c's host work on its own global stream
+            np.random.set_state(states[c])
+            try:
+                return fn()
+            finally:
+                states[c] = np.random.get_state()
+
+        def by_k(idx, fn):             # fn(list of chains with one K) per distinct K
+            groups = {}
+            for c in idx:
+                groups.setdefault(q[c].size, []).append(c)
+            for cs in groups.values():
+                fn(cs)
+
+        def energies(idx):
+            out = {}
+
+            def run(cs):
+                V = np.atleast_1d(self.V(np.stack([q[c] for c in cs]), f_pos=f_pos))
+                out.update(zip(cs, V))
+            by_k(idx, run)
+            return out
+
+        def trajectories(idx):
+            def run(cs):
+                qq, pp = self.RHMC_steps(np.stack([q[c] for c in cs]),
+                                         np.stack([p[c] for c in cs]), Nsteps, delta=delta,
+                                         counter_max=counter_max)
+                qq, pp = np.atleast_2d(qq), np.atleast_2d(pp)
+                for i, c in enumerate(cs):
+                    q[c], p[c] = qq[i], pp[i]
+            by_k(idx, run)
+
+        try:
+            for l in range(n_it):
+                if schedule_g_ff2 is not None and l < schedule_g_ff2.size:
+                    self.g_ff2 = schedule_g_ff2[l]
+                if schedule_beta is not None and l < schedule_beta.size:
+                    self.beta = schedule_beta[l]
+                everyone = range(n)
+                # momentum, move type and (for a jump) grow/shrink: :1020-1047, :1094
+                for c in everyone:
+                    def draw(c=c):
+                        H = self.H(q[c], grad=False)
+                        p[c] = self.u_sample(q[c].size) * np.sqrt(H)
+                        m = np.random.choice([0, 1, 2], p=self.P_move, size=1)[0]
+                        g = np.random.choice([True, False], p=[0.5, 0.5]) if m != 0 else False
+                        return H, m, g
+                    H, move[c], grow[c] = host(c, draw)
+                    self.T_chain[l, c] = self.T(p[c], H)
+                V0 = energies(everyone)
+                for c in everyone:
+                    d = q[c].size
+                    self.V_chain[l, c] = V0[c]
+                    E0[c] = self.E_chain[l, c] = V0[c] + self.T_chain[l, c]
+                    self.q_chain[l, c, :d], self.p_chain[l, c, :d] = q[c], p[c]
+                    self.N_chain[l, c] = d // 3
+                    self.move_chain[l, c] = (0 if move[c] == 0 else
+                                             (1 if grow[c] else 2) if move[c] == 1 else
+                                             (3 if grow[c] else 4))
+                trajectories(everyone)
+                jump = [c for c in everyone if move[c] != 0]
+                for c in jump:                              # :1096-1104, the proposal
+                    def propose(c=c):
+                        self.Nobjs, self.d = q[c].size // 3, q[c].size
+                        mv = self.birth_death_move if move[c] == 1 else self.split_merge_move
+                        return mv(q[c], -p[c], grow[c])
+                    q[c], p[c], factor[c] = host(c, propose)
+                trajectories(jump)
+                for c in jump:
+                    p[c] = -p[c]
+                V1 = energies(everyone)
+                for c in everyone:
+                    E1 = V1[c] + self.T(p[c], self.H(q[c], grad=False))
+                    u = host(c, lambda: np.log(np.random.random(1)))
+                    if move[c] == 0:                        # :1075-1083
+                        dE = E1 - E0[c]
+                        acc = (dE < 0) or (u < -dE)
+                    else:                                   # :1160-1181
+                        ln_alpha0 = -(E1 - E0[c]) + factor[c]
+                        acc = (ln_alpha0 > 0) or (u < ln_alpha0)
+                    self.A_chain[l, c] = bool(acc)
+                    if not acc:
+                        d = 3 * self.N_chain[l, c]
+                        q[c] = self.q_chain[l, c, :d].copy()
+        finally:
+            np.random.set_state(saved)
+        self.Nobjs = self.d = None
+        return q
+
     def R_accept_report(self, idx_iter, cumulative=True, running=True, run_window=10):
         """sampler_RHMC.py:1447-1473"""
         def rep(A, M):

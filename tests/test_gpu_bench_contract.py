@@ -40,6 +40,9 @@ def test_bench_json_line():
     e = d["end_to_end"]
     assert e["unit"] == d["unit"] and 0 < e["value"] <= 1.05 * d["value"]
     assert d["cpu_baseline"] is None              # --no-cpu
+    sys.path.insert(0, ROOT)
+    import bench
+    assert d["sources"] == bench.source_hash()    # the line names the sources it ran
 
 
 @pytest.mark.gpu

@@ -199,6 +199,64 @@ def test_run_RHMC_reversible_jump_moves(gpu_lib, name):
     np.testing.assert_allclose(g.E_chain, z[name + "/E_chain"], rtol=1e-11)
 
 
+def test_run_RHMC_rj_batched_equals_single_runs(gpu_lib):
+    """run_RHMC_rj_batched: chains at different, changing star counts, each on
+    its own seeded stream, with every GPU phase batched over the chains
+    (grouped by K).  Chain 0 is the reference's rj_all run (its seed and
+    start) and reproduces the golden; the others equal one run_RHMC per seed
+    (which test_run_RHMC_reversible_jump_moves pins to the reference)."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+    kw = dict(f_pos=True, delta=1e-6, Niter=int(z[name + "/niter"]),
+              Nsteps=int(z[name + "/nsteps"]), dt=float(z[name + "/dt"]),
+              N_max=int(z[name + "/N_max"]), P_move=list(z[name + "/P_move"]))
+    qm = z[name + "/q_model"]
+    seed0 = int(z[name + "/seed"])
+    # further chains: 2- and 3-star starts on seeds whose single runs complete
+    # (the reference dead-ends on some: no star left, nothing mergeable)
+    chains, singles = [(qm, seed0)], []
+    for s in range(400, 440):
+        if len(chains) == 4:
+            break
+        start = qm[:2] if len(chains) % 2 else qm
+        h = _gym(par)
+        h.D = z[name + "/D"]
+        np.random.seed(s)
+        try:
+            with np.errstate(all="ignore"):
+                h.run_RHMC(start.copy(), **kw)
+        except Exception:
+            continue
+        chains.append((start, s))
+        singles.append(h)
+    assert len(chains) == 4
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    np.random.seed(1)
+    before = np.random.get_state()[1].copy()
+    q_end = g.run_RHMC_rj_batched([c[0].copy() for c in chains], [c[1] for c in chains], **kw)
+    assert np.array_equal(np.random.get_state()[1], before)   # the global stream is untouched
+    assert len(q_end) == 4
+    # chain 0: the reference's own run
+    np.testing.assert_array_equal(g.move_chain[:, 0], z[name + "/move_chain"])
+    np.testing.assert_array_equal(g.N_chain[:, 0], z[name + "/N_chain"])
+    np.testing.assert_array_equal(g.A_chain[:, 0].astype(np.int32), z[name + "/A_chain"])
+    assert_state_close(g.q_chain[:, 0], z[name + "/q_chain"], 1e-9, "q_chain")
+    assert_state_close(g.p_chain[:, 0], z[name + "/p_chain"], 1e-9, "p_chain")
+    np.testing.assert_allclose(g.E_chain[:, 0], z[name + "/E_chain"], rtol=1e-11)
+    # the others: one run_RHMC per seed
+    for c, h in enumerate(singles, start=1):
+        np.testing.assert_array_equal(g.move_chain[:, c], h.move_chain)
+        np.testing.assert_array_equal(g.N_chain[:, c], h.N_chain)
+        np.testing.assert_array_equal(g.A_chain[:, c], h.A_chain)
+        assert_state_close(g.q_chain[:, c], h.q_chain, 1e-11, "chain %d" % c)
+        np.testing.assert_allclose(g.E_chain[:, c], h.E_chain, rtol=1e-12)
+    # the batch really mixed star counts, and some jump was accepted
+    assert len(set(g.N_chain[-1])) > 1 or len(set(g.N_chain[:, 0])) > 1
+    assert (g.move_chain[g.A_chain] > 0).any()
+
+
 def _sched_gym(z, name):
     par = R.params_from_npz(z, name + "/par_")
     g = _gym(par)
