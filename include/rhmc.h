@@ -201,7 +201,8 @@ int rhmc_ctx_synchronize(rhmc_ctx* ctx);
  * n_steps RHMC_single_step()s on every chain.  q, p: host [n_chains][3K],
  * updated in place.  fp_iters (nullable): host int32 [n_chains][2], the
  * p- and q-loop iteration counts summed over the n_steps steps.  status
- * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 64.
+ * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 256 on
+ * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).
  */
 int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p,
                   int64_t n_chains, int32_t K, int32_t n_steps,
