@@ -241,6 +241,20 @@ class base_class(object):
                 Hd[3 * i + 1] = Hd[3 * i + 2] = self.H_xx(f)
         return (Hd, Hg) if grad else Hd
 
+    def _H_vec(self, q):
+        """H(q, grad=False) with the per-star loop vectorised: the same IEEE
+        operations in the same order per element (tests/test_sampler_host.py
+        checks bit equality with H), for the batched runners' host work."""
+        f = np.asarray(q, dtype=np.float64)[0::3]
+        Hf = 1. / (f / self.g_ff2 + (self.B_count / self.g0) / self.g_ff)
+        f_low = self.mag2flux_converter(self.mB + 2)
+        fl = np.where(f < f_low, f_low, f)
+        s = 1. / (self.g1 * fl) + self.B_count / (self.g2 * fl ** 2)
+        Hx = self.g_xx * s ** -1
+        Hd = np.empty(3 * f.size)
+        Hd[0::3], Hd[1::3], Hd[2::3] = Hf, Hx, Hx
+        return Hd
+
     def H_xx(self, f, grad=False):
         """sampler_RHMC.py:260-280"""
         f_low = self.mag2flux_converter(self.mB + 2)
@@ -686,10 +700,7 @@ class multi_gym(base_class):
         self.move_chain = np.zeros((n_it, n), dtype=int)
         self.N_chain = np.zeros((n_it, n), dtype=int)
         saved = np.random.get_state()
-        states = []
-        for s in seeds:
-            np.random.seed(s)
-            states.append(np.random.get_state())
+        streams = [np.random.RandomState(s) for s in seeds]   # == np.random.seed(s)
         q = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
         p = [None] * n
         move = [0] * n
@@ -697,12 +708,12 @@ class multi_gym(base_class):
         E0 = np.zeros(n)
         factor = np.zeros(n)
 
-        def host(c, fn):               # chain c's host work on its own global stream
-            np.random.set_state(states[c])
+        def host(c, fn):               # chain c's stream as the global one (the moves'
+            np.random.set_state(streams[c].get_state())   # np.random / scipy draws)
             try:
                 return fn()
             finally:
-                states[c] = np.random.get_state()
+                streams[c].set_state(np.random.get_state())
 
         def by_k(idx, fn):             # fn(list of chains with one K) per distinct K
             groups = {}
@@ -739,13 +750,12 @@ class multi_gym(base_class):
                 everyone = range(n)
                 # momentum, move type and (for a jump) grow/shrink: :1020-1047, :1094
                 for c in everyone:
-                    def draw(c=c):
-                        H = self.H(q[c], grad=False)
-                        p[c] = self.u_sample(q[c].size) * np.sqrt(H)
-                        m = np.random.choice([0, 1, 2], p=self.P_move, size=1)[0]
-                        g = np.random.choice([True, False], p=[0.5, 0.5]) if m != 0 else False
-                        return H, m, g
-                    H, move[c], grow[c] = host(c, draw)
+                    r = streams[c]
+                    H = self._H_vec(q[c])
+                    p[c] = r.randn(q[c].size) * np.sqrt(H)          # u_sample (:1022)
+                    move[c] = r.choice([0, 1, 2], p=self.P_move, size=1)[0]
+                    grow[c] = (r.choice([True, False], p=[0.5, 0.5]) if move[c] != 0
+                               else False)
                     self.T_chain[l, c] = self.T(p[c], H)
                 V0 = energies(everyone)
                 for c in everyone:
@@ -770,8 +780,8 @@ class multi_gym(base_class):
                     p[c] = -p[c]
                 V1 = energies(everyone)
                 for c in everyone:
-                    E1 = V1[c] + self.T(p[c], self.H(q[c], grad=False))
-                    u = host(c, lambda: np.log(np.random.random(1)))
+                    E1 = V1[c] + self.T(p[c], self._H_vec(q[c]))
+                    u = np.log(streams[c].random_sample(1))
                     if move[c] == 0:                        # :1075-1083
                         dE = E1 - E0[c]
                         acc = (dE < 0) or (u < -dE)

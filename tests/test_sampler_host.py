@@ -119,3 +119,21 @@ def test_run_RHMC_verbose_report_after_move0(capsys):
     assert "Completed iteration 0" in out and "Completed iteration 50" in out
     assert out.count("N_objs: 1") == 2
     assert g.A_chain.all()                        # dE = T1 - T0 = 0 with the stubs
+
+
+def test_vectorised_H_is_bit_identical():
+    """run_RHMC_rj_batched's per-chain host work uses _H_vec: it must equal the
+    reference-order per-star H bit for bit (fluxes on both sides of the f_low
+    clamp, several metric settings)."""
+    from rhmc_amd import sampler
+    rs = np.random.RandomState(3)
+    for g_xx, g_ff, g_ff2 in ((1., 1., 1.), (0.05, 4., 4.), (10., 10., 2.)):
+        g = sampler.multi_gym(g_xx=g_xx, g_ff=g_ff, g_ff2=g_ff2)
+        f_low = g.mag2flux_converter(g.mB + 2)
+        K = 60
+        q = np.empty(3 * K)
+        q[0::3] = np.concatenate([f_low * rs.uniform(0.01, 0.999, K // 3),
+                                  f_low * rs.uniform(1.001, 1e4, K - K // 3 - 1), [f_low]])
+        q[1::3] = rs.uniform(0, 32, K)
+        q[2::3] = rs.uniform(0, 32, K)
+        assert np.array_equal(g._H_vec(q), g.H(q, grad=False))
