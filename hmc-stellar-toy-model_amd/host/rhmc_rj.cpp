@@ -1,0 +1,549 @@
+// rhmc_rj.cpp — librhmc_rj.so: multi_gym.run_RHMC's reversible-jump sampler
+// (sampler_RHMC.py:937-1198, moves :1200-1445) for many chains at once, native
+// host code around the engine's C-ABI (include/rhmc_rj.h).
+//
+// One iteration l (every chain c has its own RandomState replica and star
+// count K_c):
+//   1. host, per chain, in parallel: g_ff2 / beta from the schedules
+//      (:1010-1016), H(q) (:229-258), p = randn(3K) sqrt(H) (:1021-1022),
+//      T0 (:1026), the move type (:1045) and grow / shrink (:1094, :1140)
+//   2. engine: V(q) of every chain, grouped by K                  (:1025)
+//   3. engine: Nsteps steps on every chain, grouped by K     (:1053, :1098)
+//   4. host, jumping chains: p = -p, the proposal and its ln-acceptance
+//      factor (:1099-1102; birth_death_move / split_merge_move)
+//   5. engine: Nsteps steps on the jumping chains at their new K   (:1109)
+//   6. engine: V(q') of every chain                          (:1069, :1117)
+//   7. host: E1 = V' + T(p', H(q')), the accept uniform, accept / restore
+//      (:1072-1083, :1120-1131)
+// The host expressions follow the reference's operation order
+// (rhmc_amd/sampler.py's _H_vec / T / moves, which tests pin to it).
+#include "rhmc_rj.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "np_legacy.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+constexpr double kPi = 3.141592653589793;  // np.pi
+
+// ------------------------------------------------------------ model helpers
+// H(q) of one star (sampler.py _H_vec, sampler_RHMC.py:260-292): Hd = (H_ff,
+// H_xx, H_xx).
+struct Metric {
+  double g_ff2, g_ff, g_xx, g0, g1, g2, B, f_low;
+  void star(double f, double* Hd) const {
+    const double Hf = 1. / (f / g_ff2 + (B / g0) / g_ff);
+    const double fl = f < f_low ? f_low : f;
+    const double s = 1. / (g1 * fl) + B / (g2 * (fl * fl));
+    const double Hx = g_xx * (1. / s);
+    Hd[0] = Hf;
+    Hd[1] = Hx;
+    Hd[2] = Hx;
+  }
+  void all(const double* q, int64_t d, double* Hd) const {
+    for (int64_t i = 0; i < d; i += 3) star(q[i], Hd + i);
+  }
+};
+
+// T(p, H) = (sum p^2 / H + sum ln|H|) / 2 with NumPy's pairwise sums (:353-363)
+double kinetic(const double* p, const double* H, int64_t d, std::vector<double>& tmp) {
+  tmp.resize((size_t)d);
+  for (int64_t i = 0; i < d; ++i) tmp[i] = (p[i] * p[i]) / H[i];
+  const double s1 = rhmc_np::pairwise_sum(tmp.data(), d);
+  for (int64_t i = 0; i < d; ++i) tmp[i] = std::log(std::fabs(H[i]));
+  const double s2 = rhmc_np::pairwise_sum(tmp.data(), d);
+  return (s1 + s2) / 2.;
+}
+
+// RandomState.choice(k, p=w) for one value: cdf = cumsum(w) / cdf[-1], one
+// uniform, searchsorted(side='right')
+int64_t choice(rhmc_np::Legacy& r, const double* w, int64_t k, std::vector<double>& cdf) {
+  cdf.resize((size_t)k);
+  double acc = 0.;
+  for (int64_t i = 0; i < k; ++i) cdf[i] = acc = acc + w[i];
+  const double last = cdf[k - 1];
+  for (int64_t i = 0; i < k; ++i) cdf[i] /= last;
+  const double u = r.random_sample();
+  return std::upper_bound(cdf.begin(), cdf.end(), u) - cdf.begin();
+}
+
+// scipy.stats.beta.logpdf / pdf (xlog1py(b-1, -x) + xlogy(a-1, x) - betaln(a, b))
+double beta_logpdf(double x, double a, double b) {
+  const double lb = std::lgamma(a) + std::lgamma(b) - std::lgamma(a + b);
+  const double t1 = (b - 1.0 == 0.0) ? 0.0 : (b - 1.0) * std::log1p(-x);
+  const double t2 = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * std::log(x);
+  return t1 + t2 - lb;
+}
+double beta_pdf(double x, double a, double b) {
+  if (!(x >= 0.0 && x <= 1.0)) return 0.0;
+  return std::exp(beta_logpdf(x, a, b));
+}
+
+// ------------------------------------------------------------------- chains
+struct Chain {
+  rhmc_np::Legacy rng;
+  std::vector<double> q, p, q0;  // state, momentum, the iteration's starting q
+  int32_t K = 0, K0 = 0;
+  int move = 0;                  // 0 within, 1 birth/death, 2 split/merge
+  bool grow = false, dead = false;
+  double E0 = 0., factor = 0.;
+  std::vector<double> H, tmp, cdf;
+};
+
+struct Run {
+  const rhmc_rj_physics* phys;
+  rhmc_params P;
+  const rhmc_rj_config* cfg;
+  std::vector<Chain> ch;
+  int nt;
+  int Kmax;
+
+  template <class F>
+  void parallel(const std::vector<int64_t>& idx, F f) {
+    const int64_t n = (int64_t)idx.size();
+    if (nt <= 1 || n < 32) {
+      for (int64_t i = 0; i < n; ++i) f(idx[i]);
+      return;
+    }
+    std::atomic<int64_t> next{0};
+    auto work = [&]() {
+      for (;;) {
+        const int64_t b = next.fetch_add(16);
+        if (b >= n) return;
+        const int64_t e = std::min(n, b + 16);
+        for (int64_t i = b; i < e; ++i) f(idx[i]);
+      }
+    };
+    std::vector<std::thread> th;
+    const int m = (int)std::min<int64_t>(nt, (n + 15) / 16);
+    for (int t = 1; t < m; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+  }
+
+  // chains grouped by star count in order of first appearance
+  std::vector<std::pair<int32_t, std::vector<int64_t>>> groups(const std::vector<int64_t>& idx) {
+    std::vector<std::pair<int32_t, std::vector<int64_t>>> g;
+    std::map<int32_t, size_t> where;
+    for (int64_t c : idx) {
+      const int32_t K = ch[c].K;
+      auto it = where.find(K);
+      if (it == where.end()) {
+        where[K] = g.size();
+        g.push_back({K, {c}});
+      } else {
+        g[it->second].second.push_back(c);
+      }
+    }
+    return g;
+  }
+
+  int energies(const std::vector<int64_t>& idx, std::vector<double>& V) {
+    std::vector<double> qb, vb;
+    for (auto& grp : groups(idx)) {
+      const int32_t K = grp.first;
+      const auto& cs = grp.second;
+      const size_t d = 3 * (size_t)K;
+      qb.resize(cs.size() * d);
+      vb.assign(cs.size(), 0.);
+      for (size_t i = 0; i < cs.size(); ++i) std::memcpy(&qb[i * d], ch[cs[i]].q.data(), d * 8);
+      const int rc = phys->energy(phys->user, &P, qb.data(), (int64_t)cs.size(), K, cfg->f_pos,
+                                  vb.data());
+      if (rc != 0) return engine_fail(rc, "energy");
+      for (size_t i = 0; i < cs.size(); ++i) V[cs[i]] = vb[i];
+    }
+    return 0;
+  }
+
+  int trajectories(const std::vector<int64_t>& idx) {
+    std::vector<double> qb, pb;
+    for (auto& grp : groups(idx)) {
+      const int32_t K = grp.first;
+      const auto& cs = grp.second;
+      const size_t d = 3 * (size_t)K;
+      qb.resize(cs.size() * d);
+      pb.resize(cs.size() * d);
+      for (size_t i = 0; i < cs.size(); ++i) {
+        std::memcpy(&qb[i * d], ch[cs[i]].q.data(), d * 8);
+        std::memcpy(&pb[i * d], ch[cs[i]].p.data(), d * 8);
+      }
+      const int rc = phys->steps(phys->user, &P, qb.data(), pb.data(), (int64_t)cs.size(), K,
+                                 cfg->n_steps);
+      if (rc != 0) return engine_fail(rc, "steps");
+      for (size_t i = 0; i < cs.size(); ++i) {
+        std::memcpy(ch[cs[i]].q.data(), &qb[i * d], d * 8);
+        std::memcpy(ch[cs[i]].p.data(), &pb[i * d], d * 8);
+      }
+    }
+    return 0;
+  }
+
+  int engine_fail(int rc, const char* what) {
+    const char* m = rhmc_last_error();
+    return fail(rc, std::string("engine ") + what + " failed: " + (m ? m : ""));
+  }
+
+  Metric metric() const {
+    return Metric{P.g_ff2, P.g_ff, P.g_xx, P.g0, P.g1, P.g2, P.B_count, P.f_low};
+  }
+
+  // --------------------------------------------------------------- moves
+  // birth_death_move (sampler_RHMC.py:1200-1270) on (q, -p); false = dead end
+  bool birth_death(Chain& c, const Metric& M) {
+    const double alpha = P.alpha;
+    if (c.grow) {
+      if (c.K + 1 > Kmax) return false;
+      const double x = c.rng.random_sample() * (cfg->rows - 2.) + 1.;    // :1219
+      const double y = c.rng.random_sample() * (cfg->cols - 2.) + 1.;    // :1220
+      const double u = c.rng.random_sample();                             // :1221
+      const double e = 1 - alpha;                                         // utils.py:469-471
+      const double lm = std::pow(cfg->fmin, e) + u * (std::pow(cfg->fmax, e) - std::pow(cfg->fmin, e));
+      const double f = std::exp(std::log(lm) / e);
+      const double qn[3] = {f, x, y};
+      double H3[3], pn[3];
+      M.star(f, H3);
+      for (int i = 0; i < 3; ++i) pn[i] = c.rng.gauss() * std::sqrt(H3[i]);   // :1231
+      c.factor = alpha * std::log(f) - 3 / 2. + kinetic(pn, H3, 3, c.tmp) + P.V_prior_const;
+      c.q.insert(c.q.end(), qn, qn + 3);
+      c.p.insert(c.p.end(), pn, pn + 3);
+      c.K += 1;
+    } else {
+      if (c.K - 1 < 1) return false;
+      const int64_t k = c.rng.randint(0, c.K);                            // :1249
+      double H3[3];
+      M.star(c.q[3 * k], H3);
+      const double Tk = kinetic(&c.p[3 * k], H3, 3, c.tmp);
+      c.factor = -alpha * std::log(c.q[3 * k]) + 3 / 2. - Tk - P.V_prior_const;
+      c.q.erase(c.q.begin() + 3 * k, c.q.begin() + 3 * k + 3);
+      c.p.erase(c.p.begin() + 3 * k, c.p.begin() + 3 * k + 3);
+      c.K -= 1;
+    }
+    return true;
+  }
+
+  // split_merge_move (sampler_RHMC.py:1273-1445) on (q, -p); false = dead end
+  bool split_merge(Chain& c, const Metric& M) {
+    const double a = cfg->beta_a, b = cfg->beta_b, Ks = cfg->K_split;
+    const double two_pi_ks2 = 2 * kPi * std::pow(Ks, 2);
+    const double ln_q_dxdy = std::log(two_pi_ks2);
+    const double two_ks2 = 2 * std::pow(Ks, 2);
+    if (c.grow) {
+      if (c.K + 1 > Kmax) return false;
+      const int64_t i = c.rng.randint(0, c.K);                            // :1291
+      const double fs = c.q[3 * i], xs = c.q[3 * i + 1], ys = c.q[3 * i + 2];
+      const double qs[3] = {fs, xs, ys}, ps[3] = {c.p[3 * i], c.p[3 * i + 1], c.p[3 * i + 2]};
+      const double g1 = c.rng.gauss(), g2 = c.rng.gauss();                // :1300
+      const double dx = g1 * Ks, dy = g2 * Ks;
+      const double dr_sq = std::pow(dx, 2) + std::pow(dy, 2);
+      const double F = c.rng.beta(a, b);                                  // :1302
+      const double q1[3] = {F * fs, xs + (1 - F) * dx, ys + (1 - F) * dy};
+      const double q2[3] = {(1 - F) * fs, xs - F * dx, ys - F * dy};
+      double H1[3], H2[3], Hs[3], p1[3], p2[3];
+      M.star(q1[0], H1);
+      for (int t = 0; t < 3; ++t) p1[t] = c.rng.gauss() * std::sqrt(H1[t]);   // :1328
+      M.star(q2[0], H2);
+      for (int t = 0; t < 3; ++t) p2[t] = c.rng.gauss() * std::sqrt(H2[t]);   // :1333
+      M.star(qs[0], Hs);
+      const double Ts = kinetic(ps, Hs, 3, c.tmp);
+      const double T1 = kinetic(p1, H1, 3, c.tmp), T2 = kinetic(p2, H2, 3, c.tmp);
+      c.factor = (-3 / 2.) + std::log(fs) - beta_logpdf(F, a, b) + ln_q_dxdy + (dr_sq / two_ks2) +
+                 T1 + T2 - Ts;
+      for (int t = 0; t < 3; ++t) {
+        c.q[3 * i + t] = q1[t];
+        c.p[3 * i + t] = p1[t];
+      }
+      c.q.insert(c.q.end(), q2, q2 + 3);
+      c.p.insert(c.p.end(), p2, p2 + 3);
+      c.K += 1;
+      return true;
+    }
+    const int64_t n = c.K;
+    if (n - 1 < 1) return false;
+    // pair probabilities ~ Beta(F_ij) N(r_ij), self pairs excluded (:1366-1378)
+    std::vector<double> P2((size_t)(n * n));
+    for (int64_t r = 0; r < n; ++r)
+      for (int64_t s = 0; s < n; ++s) {
+        const double fr = c.q[3 * r], fc = c.q[3 * s];
+        const double Fm = fc / (fr + fc);
+        double v = beta_pdf(Fm, a, b);
+        if (std::fabs(Fm - 0.5) < 1e-6) v = 0.;
+        const double ddx = c.q[3 * r + 1] - c.q[3 * s + 1], ddy = c.q[3 * r + 2] - c.q[3 * s + 2];
+        const double Rsq = std::pow(ddx, 2) + std::pow(ddy, 2);
+        P2[r * n + s] = v * (std::exp(-Rsq / (2. * std::pow(Ks, 2))) / (2. * kPi * std::pow(Ks, 2)));
+      }
+    const double tot = rhmc_np::pairwise_sum(P2.data(), n * n);
+    if (!(tot > 0.0) || !std::isfinite(tot)) return false;  // the reference raises here
+    for (auto& v : P2) v /= tot;
+    const int64_t pair = choice(c.rng, P2.data(), n * n, c.cdf);          // :1381
+    if (pair >= n * n) return false;
+    const int64_t i1 = pair / n, i2 = pair % n;
+    const double q1[3] = {c.q[3 * i1], c.q[3 * i1 + 1], c.q[3 * i1 + 2]};
+    const double p1[3] = {c.p[3 * i1], c.p[3 * i1 + 1], c.p[3 * i1 + 2]};
+    const double q2[3] = {c.q[3 * i2], c.q[3 * i2 + 1], c.q[3 * i2 + 2]};
+    const double p2[3] = {c.p[3 * i2], c.p[3 * i2 + 1], c.p[3 * i2 + 2]};
+    const double F = q1[0] / (q1[0] + q2[0]);
+    const double dx = q1[1] - q2[1], dy = q1[2] - q2[2];
+    const double dr_sq = std::pow(dx, 2) + std::pow(dy, 2);
+    const double qs[3] = {q1[0] + q2[0], F * q1[1] + (1 - F) * q2[1], F * q1[2] + (1 - F) * q2[2]};
+    double H1[3], H2[3], Hs[3], ps[3];
+    M.star(q1[0], H1);
+    const double T1 = kinetic(p1, H1, 3, c.tmp);
+    M.star(q2[0], H2);
+    const double T2 = kinetic(p2, H2, 3, c.tmp);
+    M.star(qs[0], Hs);
+    for (int t = 0; t < 3; ++t) ps[t] = c.rng.gauss() * std::sqrt(Hs[t]);      // :1415
+    const double Ts = kinetic(ps, Hs, 3, c.tmp);
+    const int64_t lo = std::min(i1, i2), hi = std::max(i1, i2);
+    std::vector<double> nq, np_;
+    nq.reserve((size_t)(3 * (n - 1)));
+    np_.reserve((size_t)(3 * (n - 1)));
+    for (int64_t s = 0; s < n; ++s) {
+      if (s == lo || s == hi) continue;
+      nq.insert(nq.end(), &c.q[3 * s], &c.q[3 * s] + 3);
+      np_.insert(np_.end(), &c.p[3 * s], &c.p[3 * s] + 3);
+    }
+    nq.insert(nq.end(), qs, qs + 3);
+    np_.insert(np_.end(), ps, ps + 3);
+    c.factor = (3 / 2.) - std::log(qs[0]) + beta_logpdf(F, a, b) - ln_q_dxdy - (dr_sq / two_ks2) -
+               T1 - T2 + Ts;
+    c.q.swap(nq);
+    c.p.swap(np_);
+    c.K -= 1;
+    return true;
+  }
+};
+
+int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, const int32_t* K,
+          const uint32_t* seeds, int64_t n) {
+  if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
+  if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
+  if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
+  if (n > 0 && (!q || !K || !seeds)) return fail(RHMC_ERR_ARG, "q, K or seeds is NULL");
+  if (cfg->n_iter < 0 || cfg->n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter or n_steps < 0");
+  if (cfg->N_max < 1 || cfg->N_max > 256) return fail(RHMC_ERR_ARG, "N_max must be in [1, 256]");
+  if (cfg->rows < 3 || cfg->cols < 3) return fail(RHMC_ERR_ARG, "rows / cols < 3");
+  if ((cfg->n_g_ff2 > 0 && !cfg->schedule_g_ff2) || (cfg->n_beta > 0 && !cfg->schedule_beta) ||
+      cfg->n_g_ff2 < 0 || cfg->n_beta < 0)
+    return fail(RHMC_ERR_ARG, "schedule array missing");
+  double ps = 0.;
+  for (int i = 0; i < 3; ++i) {
+    if (!(cfg->P_move[i] >= 0.0)) return fail(RHMC_ERR_ARG, "P_move entries must be >= 0");
+    ps += cfg->P_move[i];
+  }
+  if (!(std::fabs(ps - 1.0) <= 1.4901161193847656e-08))  // choice(): sqrt(eps) tolerance
+    return fail(RHMC_ERR_ARG, "P_move must sum to 1");
+  if ((cfg->P_move[1] > 0 || cfg->P_move[2] > 0) &&
+      !(cfg->fmin > 0 && cfg->fmax > 0 && cfg->K_split > 0 && cfg->beta_a > 0 && cfg->beta_b > 0))
+    return fail(RHMC_ERR_ARG, "jumps need fmin, fmax, K_split, beta_a, beta_b > 0");
+  for (int64_t c = 0; c < n; ++c)
+    if (K[c] < 1 || K[c] > cfg->N_max) return fail(RHMC_ERR_ARG, "K[c] must be in [1, N_max]");
+  return 0;
+}
+
+int run(const rhmc_rj_physics* phys, const rhmc_params* P0, const rhmc_rj_config* cfg,
+        double* q, int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
+  if (int rc = check(P0, cfg, q, K, seeds, n)) return rc;
+  if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
+  Run R;
+  R.phys = phys;
+  R.P = *P0;
+  R.cfg = cfg;
+  R.Kmax = cfg->N_max;
+  int nt = cfg->n_threads;
+  if (nt <= 0) nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+  R.nt = nt;
+  R.ch.resize((size_t)n);
+  const int64_t W = 3 * (int64_t)cfg->N_max;
+  std::vector<int64_t> all((size_t)n);
+  for (int64_t c = 0; c < n; ++c) {
+    all[c] = c;
+    Chain& h = R.ch[c];
+    h.rng.seed(seeds[c]);
+    h.K = K[c];
+    h.q.assign(q + c * W, q + c * W + 3 * (int64_t)K[c]);
+  }
+  const int64_t rows_n = (int64_t)cfg->n_iter + 1;
+  std::vector<double> V0((size_t)n), V1((size_t)n), T0((size_t)n);
+  for (int64_t l = 0; l < rows_n; ++l) {
+    if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
+    if (cfg->n_beta > 0) R.P.beta = cfg->schedule_beta[std::min<int64_t>(l, cfg->n_beta - 1)];
+    const Metric M = R.metric();
+    // 1. momentum, T0, move type, grow / shrink
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      const int64_t d = 3 * (int64_t)h.K;
+      h.H.resize((size_t)d);
+      M.all(h.q.data(), d, h.H.data());
+      h.p.resize((size_t)d);
+      for (int64_t i = 0; i < d; ++i) h.p[i] = h.rng.gauss() * std::sqrt(h.H[i]);
+      h.move = (int)choice(h.rng, cfg->P_move, 3, h.cdf);
+      h.grow = false;
+      if (h.move != 0) {
+        const double half[2] = {0.5, 0.5};
+        h.grow = choice(h.rng, half, 2, h.cdf) == 0;   // [True, False]
+      }
+      T0[c] = kinetic(h.p.data(), h.H.data(), d, h.tmp);
+      h.q0 = h.q;
+      h.K0 = h.K;
+      h.dead = false;
+    });
+    // 2. V(q)
+    if (int rc = R.energies(all, V0)) return rc;
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      h.E0 = V0[c] + T0[c];
+      const int64_t r = l * n + c;
+      if (rec) {
+        if (rec->q_chain) {
+          double* row = rec->q_chain + r * W;
+          std::fill(row, row + W, 0.);
+          std::copy(h.q.begin(), h.q.end(), row);
+        }
+        if (rec->p_chain) {
+          double* row = rec->p_chain + r * W;
+          std::fill(row, row + W, 0.);
+          std::copy(h.p.begin(), h.p.end(), row);
+        }
+        if (rec->V_chain) rec->V_chain[r] = V0[c];
+        if (rec->T_chain) rec->T_chain[r] = T0[c];
+        if (rec->E_chain) rec->E_chain[r] = h.E0;
+        if (rec->n_stars) rec->n_stars[r] = h.K;
+        if (rec->move)
+          rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
+      }
+    });
+    // 3. the trajectory of every chain
+    if (int rc = R.trajectories(all)) return rc;
+    // 4. the proposals
+    std::vector<int64_t> jump;
+    for (int64_t c = 0; c < n; ++c)
+      if (R.ch[c].move != 0) jump.push_back(c);
+    R.parallel(jump, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      for (auto& v : h.p) v = -v;
+      const bool ok = h.move == 1 ? R.birth_death(h, M) : R.split_merge(h, M);
+      if (!ok) {
+        h.dead = true;
+        h.q = h.q0;
+        h.K = h.K0;
+      }
+    });
+    std::vector<int64_t> live;
+    for (int64_t c : jump)
+      if (!R.ch[c].dead) live.push_back(c);
+    // 5. the trajectory after the jump
+    if (int rc = R.trajectories(live)) return rc;
+    for (int64_t c : live)
+      for (auto& v : R.ch[c].p) v = -v;
+    // 6. V(q')
+    std::vector<int64_t> scored;
+    for (int64_t c = 0; c < n; ++c)
+      if (!R.ch[c].dead) scored.push_back(c);
+    if (int rc = R.energies(scored, V1)) return rc;
+    // 7. accept / reject
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      const int64_t r = l * n + c;
+      bool acc = false;
+      if (!h.dead) {
+        const int64_t d = 3 * (int64_t)h.K;
+        h.H.resize((size_t)d);
+        M.all(h.q.data(), d, h.H.data());
+        const double E1 = V1[c] + kinetic(h.p.data(), h.H.data(), d, h.tmp);
+        const double u = std::log(h.rng.random_sample());
+        if (h.move == 0) {
+          const double dE = E1 - h.E0;
+          acc = (dE < 0) || (u < -dE);
+        } else {
+          const double ln_alpha0 = -(E1 - h.E0) + h.factor;
+          acc = (ln_alpha0 > 0) || (u < ln_alpha0);
+        }
+        if (!acc) {
+          h.q = h.q0;
+          h.K = h.K0;
+        }
+      }
+      if (rec) {
+        if (rec->accept) rec->accept[r] = acc ? 1 : 0;
+        if (rec->flags) rec->flags[r] = h.dead ? (int32_t)RHMC_RJ_DEAD_END : 0;
+      }
+    });
+  }
+  for (int64_t c = 0; c < n; ++c) {
+    const Chain& h = R.ch[c];
+    std::fill(q + c * W, q + (c + 1) * W, 0.);
+    std::copy(h.q.begin(), h.q.end(), q + c * W);
+    K[c] = h.K;
+  }
+  return 0;
+}
+
+// the engine as physics
+int ctx_energy(void* user, const rhmc_params* P, const double* q, int64_t n, int32_t K,
+               int32_t f_pos, double* V) {
+  return rhmc_energy(static_cast<rhmc_ctx*>(user), P, q, nullptr, V, nullptr, n, K, f_pos);
+}
+int ctx_steps(void* user, const rhmc_params* P, double* q, double* p, int64_t n, int32_t K,
+              int32_t n_steps) {
+  return rhmc_leapfrog(static_cast<rhmc_ctx*>(user), P, q, p, n, K, n_steps, nullptr, nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
+                        const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds,
+                        int64_t n, const rhmc_rj_record* rec) {
+  try {
+    return run(phys, P, cfg, q, K, seeds, n, rec);
+  } catch (const std::exception& e) {
+    return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
+  }
+}
+
+int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, double* q,
+                int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  rhmc_rj_physics phys{ctx, ctx_energy, ctx_steps};
+  return rhmc_rj_run_physics(&phys, P, cfg, q, K, seeds, n, rec);
+}
+
+int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, double* out) {
+  if (n < 0 || (n > 0 && !out)) return fail(RHMC_ERR_ARG, "bad n or out");
+  rhmc_np::Legacy r(seed);
+  for (int64_t i = 0; i < n; ++i) {
+    switch (kind) {
+      case 0: out[i] = r.random_sample(); break;
+      case 1: out[i] = r.gauss(); break;
+      case 2:
+        if (!(a >= 1.0)) return fail(RHMC_ERR_ARG, "randint needs a >= 1");
+        out[i] = (double)r.randint(0, (int64_t)a);
+        break;
+      case 3: out[i] = r.beta(a, b); break;
+      case 4: out[i] = r.standard_gamma(a); break;
+      case 5: out[i] = r.standard_exponential(); break;
+      default: return fail(RHMC_ERR_ARG, "unknown kind");
+    }
+  }
+  return 0;
+}
+
+const char* rhmc_rj_last_error(void) { return g_err.c_str(); }
+
+}  // extern "C"

@@ -1,0 +1,178 @@
+"""ctypes binding of librhmc_rj.so (include/rhmc_rj.h): multi_gym.run_RHMC's
+reversible-jump sampler (sampler_RHMC.py:937-1198, :1200-1445) for many
+chains, native host code around the engine.
+
+Like capi, the library is required: importing this module without a built
+librhmc_rj.so raises (build: __graft_entry__.build() or
+`make -C hmc-stellar-toy-model_amd/host`).
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import capi
+
+LIB_PATH = os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so")
+DEAD_END = 1                 # RHMC_RJ_DEAD_END
+
+EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_last_error")
+
+ENERGY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
+                             ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int32,
+                             ctypes.c_int32, ctypes.POINTER(ctypes.c_double))
+STEPS_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
+                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_double),
+                            ctypes.c_int64, ctypes.c_int32, ctypes.c_int32)
+
+
+class RjPhysics(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("energy", ENERGY_FN), ("steps", STEPS_FN)]
+
+
+class RjConfig(ctypes.Structure):
+    """Mirror of `rhmc_rj_config`."""
+    _fields_ = [("n_iter", ctypes.c_int32), ("n_steps", ctypes.c_int32),
+                ("N_max", ctypes.c_int32), ("f_pos", ctypes.c_int32),
+                ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
+                ("n_threads", ctypes.c_int32), ("n_g_ff2", ctypes.c_int32),
+                ("n_beta", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("P_move", ctypes.c_double * 3), ("fmin", ctypes.c_double),
+                ("fmax", ctypes.c_double), ("K_split", ctypes.c_double),
+                ("beta_a", ctypes.c_double), ("beta_b", ctypes.c_double),
+                ("schedule_g_ff2", ctypes.c_void_p), ("schedule_beta", ctypes.c_void_p)]
+
+
+class RjRecord(ctypes.Structure):
+    """Mirror of `rhmc_rj_record`."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("q_chain", "p_chain", "E_chain", "V_chain",
+                                                "T_chain", "accept", "move", "n_stars", "flags")]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("librhmc_rj.so not built at %s — run __graft_entry__.build()" % LIB_PATH)
+    lib = ctypes.CDLL(LIB_PATH)
+    P = ctypes.POINTER
+    vp = ctypes.c_void_p
+    sig = {
+        "rhmc_rj_run": [vp, P(capi.RhmcParams), P(RjConfig), vp, vp, vp, ctypes.c_int64,
+                        P(RjRecord)],
+        "rhmc_rj_run_physics": [P(RjPhysics), P(capi.RhmcParams), P(RjConfig), vp, vp, vp,
+                                ctypes.c_int64, P(RjRecord)],
+        "rhmc_np_draws": [ctypes.c_uint32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
+                          ctypes.c_int64, vp],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = ctypes.c_int
+        fn.argtypes = args
+    lib.rhmc_rj_last_error.restype = ctypes.c_char_p
+    lib.rhmc_rj_last_error.argtypes = []
+    return lib
+
+
+_lib = _load()
+
+
+def lib():
+    return _lib
+
+
+def _check(rc):
+    if rc != capi.RHMC_OK:
+        raise capi.RhmcError(rc, _lib.rhmc_rj_last_error().decode(errors="replace"))
+
+
+def np_draws(seed, kind, n, a=0., b=0.):
+    """n draws of RandomState(seed): kind "random_sample", "randn", "randint"
+    (randint(0, a)), "beta" (a, b), "standard_gamma" (a) or
+    "standard_exponential" — the replica's stream, for parity checks."""
+    kinds = {"random_sample": 0, "randn": 1, "randint": 2, "beta": 3, "standard_gamma": 4,
+             "standard_exponential": 5}
+    out = np.empty(int(n))
+    _check(_lib.rhmc_np_draws(int(seed), kinds[kind], float(a), float(b), int(n),
+                              out.ctypes.data))
+    return out
+
+
+def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
+        K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
+        n_threads=0):
+    """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
+    vectors.  Either ctx (a capi.Context: the engine) or physics (a pair of
+    Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
+    -> None, in place; for stand-ins).  Returns (q list, record dict)."""
+    n = len(q_models)
+    if len(seeds) != n:
+        raise ValueError("one seed per chain")
+    W = 3 * int(N_max)
+    q = np.zeros((n, W))
+    K = np.empty(n, dtype=np.int32)
+    for c, qm in enumerate(q_models):
+        qm = np.asarray(qm, dtype=np.float64).ravel()
+        if qm.size % 3 or qm.size // 3 > N_max:
+            raise ValueError("chain %d: %d values for N_max %d" % (c, qm.size, N_max))
+        q[c, :qm.size] = qm
+        K[c] = qm.size // 3
+    sd = np.asarray(seeds, dtype=np.int64)
+    if sd.size and (sd.min() < 0 or sd.max() > 2 ** 32 - 1):
+        raise ValueError("seeds must be in [0, 2**32)")
+    sd = sd.astype(np.uint32)
+    keep = []
+
+    def arr(a):
+        if a is None or np.size(a) == 0:
+            return None, 0
+        a = np.ascontiguousarray(np.ravel(a), dtype=np.float64)
+        keep.append(a)
+        return a.ctypes.data, a.size
+    sg, ng = arr(schedule_g_ff2)
+    sb, nb = arr(schedule_beta)
+    pm = (ctypes.c_double * 3)(*[float(v) for v in P_move])
+    cfg = RjConfig(int(n_iter), int(n_steps), int(N_max), int(f_pos), int(rows), int(cols),
+                   int(n_threads), ng, nb, 0, pm, float(fmin), float(fmax), float(K_split),
+                   float(beta_a), float(beta_b), sg, sb)
+    rows_n = int(n_iter) + 1
+    rec = {"q_chain": np.zeros((rows_n, n, W)), "p_chain": np.zeros((rows_n, n, W)),
+           "E_chain": np.zeros((rows_n, n)), "V_chain": np.zeros((rows_n, n)),
+           "T_chain": np.zeros((rows_n, n)), "accept": np.zeros((rows_n, n), np.int32),
+           "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),
+           "flags": np.zeros((rows_n, n), np.int32)}
+    r = RjRecord(*[rec[k].ctypes.data for k in ("q_chain", "p_chain", "E_chain", "V_chain",
+                                                  "T_chain", "accept", "move", "n_stars",
+                                                  "flags")])
+    if ctx is not None:
+        _check(_lib.rhmc_rj_run(ctx._h, ctypes.byref(params), ctypes.byref(cfg), q.ctypes.data,
+                                K.ctypes.data, sd.ctypes.data, n, ctypes.byref(r)))
+    else:
+        energy_py, steps_py = physics
+        err = []
+
+        def energy(user, P, qp, m, k, fp, Vp):
+            try:
+                qa = np.ctypeslib.as_array(qp, shape=(m, 3 * k))
+                Va = np.ctypeslib.as_array(Vp, shape=(m,))
+                Va[:] = energy_py(qa.copy(), fp)
+                return 0
+            except Exception as e:   # noqa: BLE001 - reported after the run
+                err.append(e)
+                return capi.RHMC_ERR_ARG
+
+        def steps(user, P, qp, pp, m, k, ns):
+            try:
+                qa = np.ctypeslib.as_array(qp, shape=(m, 3 * k))
+                pa = np.ctypeslib.as_array(pp, shape=(m, 3 * k))
+                steps_py(qa, pa, ns)
+                return 0
+            except Exception as e:   # noqa: BLE001
+                err.append(e)
+                return capi.RHMC_ERR_ARG
+        phys = RjPhysics(None, ENERGY_FN(energy), STEPS_FN(steps))
+        rc = _lib.rhmc_rj_run_physics(ctypes.byref(phys), ctypes.byref(params),
+                                      ctypes.byref(cfg), q.ctypes.data, K.ctypes.data,
+                                      sd.ctypes.data, n, ctypes.byref(r))
+        if err:
+            raise err[0]
+        _check(rc)
+    return [q[c, :3 * K[c]].copy() for c in range(n)], rec

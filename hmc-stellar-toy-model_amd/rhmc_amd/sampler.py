@@ -671,7 +671,8 @@ class multi_gym(base_class):
 
     def run_RHMC_rj_batched(self, q_models_0, seeds, f_pos=True, delta=1e-6, Niter=100,
                             Nsteps=100, dt=1e-1, counter_max=1000, N_max=50,
-                            P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None):
+                            P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None,
+                            engine="native", n_threads=0):
         """Many independent chains of run_RHMC WITH the reversible-jump moves
         (sampler_RHMC.py:937-1198; birth_death_move :1200-1270, split_merge_move
         :1273-1445), each chain at its own, changing, star count.  Chain c is
@@ -686,10 +687,23 @@ class multi_gym(base_class):
         q_models_0: a list of [K_c, 3] (mag, x, y) arrays.  Returns a list of
         the chains' final q; sets q_chain / p_chain [Niter+1, n, 3 N_max],
         E/V/T_chain, A_chain, move_chain, N_chain [Niter+1, n] (iteration-major,
-        like run_RHMC_batched)."""
+        like run_RHMC_batched).
+
+        engine="native" (default) runs the same algorithm in librhmc_rj.so
+        (include/rhmc_rj.h): per-chain host work in C++ on n_threads host
+        threads (0: up to 16) with a bit-identical replica of each chain's
+        NumPy stream, and flag_chain [Niter+1, n] marks the iterations whose
+        proposal was a dead end (see the header); engine="python" is the NumPy
+        loop below (the reference's own draws through np.random)."""
         n = len(q_models_0)
         if len(seeds) != n:
             raise ValueError("one seed per chain")
+        if engine == "native":
+            return self._rj_native(q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt,
+                                   counter_max, N_max, P_move, schedule_g_ff2, schedule_beta,
+                                   n_threads)
+        if engine != "python":
+            raise ValueError("engine must be 'native' or 'python'")
         self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
         self.P_move, self.N_max = P_move, N_max
         n_it = Niter + 1
@@ -796,6 +810,36 @@ class multi_gym(base_class):
             np.random.set_state(saved)
         self.Nobjs = self.d = None
         return q
+
+    def _rj_native(self, q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt, counter_max, N_max,
+                   P_move, schedule_g_ff2, schedule_beta, n_threads):
+        """run_RHMC_rj_batched through librhmc_rj.so (rhmc_rj_run)."""
+        from . import rj_native
+        self._check_geometry()
+        self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
+        self.P_move, self.N_max = P_move, N_max
+        jumps = P_move[1] != 0 or P_move[2] != 0
+        if jumps and (self.alpha is None or self.fmin is None or self.fmax is None):
+            assert False                                  # :1205-1207 (prior required)
+        q0 = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
+        P = self._params(delta, counter_max, for_energy=True)
+        q_end, rec = rj_native.run(
+            P, q0, seeds, Niter, Nsteps, N_max, P_move, capi.V_FLUX_WALL if f_pos else 0,
+            self.num_rows, self.num_cols, self.fmin if jumps else 1., self.fmax if jumps else 1.,
+            self.K_split, self.beta_a, self.beta_b, schedule_g_ff2=schedule_g_ff2,
+            schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads)
+        n_it = Niter + 1
+        for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):
+            if sched is not None and np.size(sched) > 0:    # the value of the last iteration
+                setattr(self, name, float(np.ravel(sched)[min(n_it, np.size(sched)) - 1]))
+        self.q_chain, self.p_chain = rec["q_chain"], rec["p_chain"]
+        self.E_chain, self.V_chain, self.T_chain = rec["E_chain"], rec["V_chain"], rec["T_chain"]
+        self.A_chain = rec["accept"].astype(bool)
+        self.move_chain = rec["move"].astype(int)
+        self.N_chain = rec["n_stars"].astype(int)
+        self.flag_chain = rec["flags"]
+        self.Nobjs = self.d = None
+        return q_end
 
     def R_accept_report(self, idx_iter, cumulative=True, running=True, run_window=10):
         """sampler_RHMC.py:1447-1473"""

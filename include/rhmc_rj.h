@@ -1,0 +1,126 @@
+/*
+ * rhmc_rj.h — C-ABI of librhmc_rj.so: the reversible-jump MCMC driver of the
+ * reference, multi_gym.run_RHMC with P_move[1:] != 0 (sampler_RHMC.py:937-1198;
+ * birth_death_move :1200-1270, split_merge_move :1273-1445), run natively for
+ * many independent chains at once around the engine of rhmc.h.
+ *
+ * Chain c is run_RHMC after np.random.seed(seeds[c]): its random numbers come
+ * from its own replica of NumPy's legacy RandomState (MT19937 with the legacy
+ * normal / gamma / beta / bounded-integer algorithms), drawn in the
+ * reference's order — momentum randn(3K) (:1021-1022), the move-type choice
+ * (:1045), the grow/shrink choice (:1094, :1140), the move's own draws
+ * (:1219-1221, :1231, :1249, :1291, :1300-1302, :1328, :1333, :1415) and the
+ * accept uniform (:1075, :1164) — so the draws are the reference's bit for
+ * bit.  The per-chain host work (metric, kinetic energy, the proposals and
+ * their ln-acceptance factors) runs on a pool of host threads; every
+ * trajectory and potential of an iteration phase is one engine call per
+ * distinct star count (chains grouped by K in order of first appearance,
+ * ascending chain index inside a group — the grouping of the Python
+ * multi_gym.run_RHMC_rj_batched, so both see identical engine batches).
+ *
+ * Replaces: the per-chain Python loop of run_RHMC's reversible-jump branches
+ * (one chain, one star count at a time) — this is its batched, native form.
+ *
+ * Where the reference itself cannot continue (a death or merge that would
+ * leave no star, a birth or split beyond N_max, a merge whose pair
+ * probabilities are all zero — the reference raises there), the proposal is
+ * rejected: the chain returns to the iteration's starting state, the rest of
+ * the move's draws and the accept uniform are not drawn, and the iteration's
+ * record gets RHMC_RJ_DEAD_END in `flags`.
+ *
+ * Arithmetic: the random draws are bit-identical to NumPy's; the metric and
+ * kinetic-energy expressions follow the reference's operation order, with
+ * C libm log/exp where NumPy may use its own SIMD versions (a last-bit
+ * difference is possible there; tests/test_rj_native_host.py bounds it).
+ *
+ * Errors: 0 or a negative RHMC_ERR_* code (rhmc.h); rhmc_rj_last_error()
+ * gives a thread-local message (an engine failure copies the engine's
+ * last-error message).
+ */
+#ifndef RHMC_RJ_H
+#define RHMC_RJ_H
+
+#include <stdint.h>
+
+#include "rhmc.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* The engine work of a run: the energy V(q) (rhmc_energy's V, f_pos bits) of
+ * n chains of K stars, and n_steps RHMC_single_step()s on them (rhmc_leapfrog,
+ * q and p updated in place).  Host arrays [n][3K].  Return 0 or a negative
+ * code.  rhmc_rj_run wires them to a context; rhmc_rj_run_physics takes any
+ * implementation (tests use stand-ins; the call order is deterministic). */
+typedef struct rhmc_rj_physics {
+  void* user;
+  int (*energy)(void* user, const rhmc_params* P, const double* q, int64_t n, int32_t K,
+                int32_t f_pos, double* V);
+  int (*steps)(void* user, const rhmc_params* P, double* q, double* p, int64_t n, int32_t K,
+               int32_t n_steps);
+} rhmc_rj_physics;
+
+typedef struct rhmc_rj_config {
+  int32_t n_iter;        /* Niter: iterations 0 .. n_iter (n_iter + 1 records)      */
+  int32_t n_steps;       /* Nsteps per trajectory                                    */
+  int32_t N_max;         /* record width 3 N_max; star counts stay in [1, N_max]     */
+  int32_t f_pos;         /* V's f_pos bits (RHMC_V_FLUX_WALL = run_RHMC f_pos=True)  */
+  int32_t rows, cols;    /* num_rows / num_cols (birth positions, :1219-1220)       */
+  int32_t n_threads;     /* host worker threads; <= 0: min(hardware threads, 16)    */
+  int32_t n_g_ff2;       /* schedule_g_ff2 length (0: none)                          */
+  int32_t n_beta;        /* schedule_beta length (0: none)                           */
+  int32_t reserved;      /* must be 0                                                */
+  double P_move[3];      /* within / birth-death / split-merge probabilities         */
+  double fmin, fmax;     /* power-law flux prior range, counts (:1221)               */
+  double K_split;        /* split offset scale (:1300)                               */
+  double beta_a, beta_b; /* split fraction F ~ Beta(beta_a, beta_b) (:1302)          */
+  const double* schedule_g_ff2;  /* iteration l: g_ff2 = s[min(l, n - 1)] (:1010-1013) */
+  const double* schedule_beta;   /* likewise beta (:1014-1016)                        */
+} rhmc_rj_config;
+
+/* Per-iteration records, row l = the state at the START of iteration l
+ * (run_RHMC's q_chain / p_chain / E_chain / V_chain / T_chain / N_chain /
+ * move_chain / A_chain, :980-1003), iteration-major.  All nullable. */
+typedef struct rhmc_rj_record {
+  double* q_chain;   /* [n_iter+1][n][3 N_max], zero past the chain's 3K */
+  double* p_chain;   /* [n_iter+1][n][3 N_max]                            */
+  double* E_chain;   /* [n_iter+1][n]                                     */
+  double* V_chain;
+  double* T_chain;
+  int32_t* accept;   /* A_chain                                           */
+  int32_t* move;     /* 0 within, 1 birth, 2 death, 3 split, 4 merge      */
+  int32_t* n_stars;  /* N_chain                                           */
+  int32_t* flags;    /* RHMC_RJ_* bits of the iteration                   */
+} rhmc_rj_record;
+
+#define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */
+
+/*
+ * Run n_iter + 1 iterations on n chains.  q: host [n][3 N_max], chain c's
+ * first 3 K[c] entries (flux in counts, x, y per star; format_q); K: [n]
+ * star counts, 1 <= K[c] <= N_max <= 256.  Both are updated in place to the
+ * chains' final states.  seeds: [n] (np.random.seed values, < 2^32).
+ * P: the engine parameters (g_ff2 / beta replaced per iteration by the
+ * schedules; V_prior_const must be set; use_prior selects the prior term of
+ * V, while the moves always use alpha, fmin, fmax as the reference does).
+ */
+int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, double* q,
+                int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec);
+int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
+                        const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds,
+                        int64_t n, const rhmc_rj_record* rec);
+
+/* The NumPy legacy stream replica, for parity checks: n draws from
+ * RandomState(seed) of `kind` into out.  kind 0: random_sample(); 1: randn();
+ * 2: randint(0, (int64)a); 3: beta(a, b); 4: standard_gamma(a);
+ * 5: standard_exponential(). */
+int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, double* out);
+
+const char* rhmc_rj_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RHMC_RJ_H */

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--chains", type=int, default=256)
     ap.add_argument("--niter", type=int, default=6)
     ap.add_argument("--nsteps", type=int, default=20)
+    ap.add_argument("--engine", choices=("native", "python"), default="native")
+    ap.add_argument("--threads", type=int, default=0, help="native host threads (0: up to 16)")
     args = ap.parse_args()
     wl = workloads.make("B4", n_chains=args.chains)
     g = sampler.multi_gym(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
@@ -42,7 +44,7 @@ def main():
         q[:, 0] = g.flux2mag_converter(q[:, 0])
         starts.append(q)
     gpu = {"s": 0.0, "calls": 0}
-    for name in ("V", "RHMC_steps"):                # time the batched GPU calls
+    for name in (("V", "RHMC_steps") if args.engine == "python" else ()):  # time GPU calls
         f = getattr(g, name)
 
         def timed(*a, _f=f, **k):
@@ -55,20 +57,23 @@ def main():
         setattr(g, name, timed)
     # warm-up (context, kernels) on two chains
     g.run_RHMC_rj_batched(starts[:2], [0, 1], Niter=1, Nsteps=2, dt=0.05, N_max=120,
-                          P_move=[0.6, 0.2, 0.2])
+                          P_move=[0.6, 0.2, 0.2], engine=args.engine, n_threads=args.threads)
     gpu["s"], gpu["calls"] = 0.0, 0
     t0 = time.perf_counter()
     g.run_RHMC_rj_batched(starts, list(range(args.chains)), Niter=args.niter,
-                          Nsteps=args.nsteps, dt=0.05, N_max=120, P_move=[0.6, 0.2, 0.2])
+                          Nsteps=args.nsteps, dt=0.05, N_max=120, P_move=[0.6, 0.2, 0.2],
+                          engine=args.engine, n_threads=args.threads)
     wall = time.perf_counter() - t0
     moves = g.move_chain
     steps = int(np.sum(np.where(moves == 0, 1, 2))) * args.nsteps
     out = {"what": "run_RHMC_rj_batched, big-sim4 geometry (32x32, K0 = 51), P_move "
                    "[0.6, 0.2, 0.2], one seeded stream per chain",
-           "chains": args.chains, "iterations": args.niter + 1, "nsteps": args.nsteps,
+           "engine": args.engine, "chains": args.chains, "iterations": args.niter + 1,
+           "nsteps": args.nsteps,
            "wall_s": wall, "ms_per_iteration": wall / (args.niter + 1) * 1e3,
            "chain_leapfrog_steps_per_s": steps / wall,
-           "gpu_call_share": gpu["s"] / wall, "gpu_calls": gpu["calls"],
+           "gpu_call_share": gpu["s"] / wall if args.engine == "python" else None,
+           "gpu_calls": gpu["calls"] if args.engine == "python" else None,
            "accepted_jumps": int(np.sum(g.A_chain & (moves > 0))),
            "star_count_range_end": [int(g.N_chain[-1].min()), int(g.N_chain[-1].max())]}
     print(json.dumps(out))

@@ -1,0 +1,108 @@
+"""The native reversible-jump driver (librhmc_rj.so, include/rhmc_rj.h) on
+the GPU against the NumPy loop of multi_gym.run_RHMC_rj_batched: both drive
+the same engine batches (chains grouped by star count), so the move types,
+star counts and accept decisions must be identical and the chains equal to
+within the last-ulp differences of the host kinetic energy (C libm's log vs
+NumPy's).  The reference pin is test_gpu_sampler.py::
+test_run_RHMC_rj_batched_equals_single_runs[native] (chain 0 = the
+reference's own rj_all run, tests/golden/rj.npz)."""
+import warnings
+
+import numpy as np
+import pytest
+
+from conftest import load_golden
+from helpers import assert_state_close
+from oracle import rhmc_ref as R
+from test_gpu_sampler import _gym
+
+pytestmark = pytest.mark.gpu
+
+
+def _starts(qm, n, rs):
+    """n starts around the golden's stars: 2-5 stars each, positions jittered."""
+    out = []
+    for c in range(n):
+        k = 2 + c % 4
+        m = np.tile(qm, (2, 1))[:k].copy()
+        m[:, 0] += rs.uniform(-0.5, 0.5, k)
+        m[:, 1:] += rs.uniform(-2, 2, (k, 2))
+        out.append(m)
+    return out
+
+
+def _completing(g_factory, starts, seeds, kw):
+    """(start, seed) pairs whose NumPy run completes: the reference raises on
+    dead ends (no star left, nothing mergeable), where the native driver
+    rejects — test_native_dead_ends_on_the_engine covers those."""
+    from rhmc_amd import capi
+    ok = []
+    for m, s in zip(starts, seeds):
+        g = g_factory()
+        with warnings.catch_warnings(), np.errstate(all="ignore"):
+            warnings.simplefilter("ignore")
+            try:
+                g.run_RHMC_rj_batched([m.copy()], [s], engine="python", **kw)
+            except (ValueError, capi.RhmcError):
+                continue
+        ok.append((m, s))
+    return ok
+
+
+@pytest.mark.parametrize("sched", [False, True])
+def test_native_equals_numpy_loop_many_chains(gpu_lib, sched):
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+
+    def make():
+        g = _gym(par)
+        g.D = z[name + "/D"]
+        return g
+    rs = np.random.RandomState(5)
+    starts = _starts(z[name + "/q_model"], 40, rs)
+    seeds = list(range(700, 740))
+    kw = dict(f_pos=True, delta=1e-6, Niter=12, Nsteps=6, dt=0.05, N_max=10,
+              P_move=[0.4, 0.3, 0.3])
+    if sched:
+        kw["schedule_g_ff2"] = np.array([1.0, 2.0, 3.0, 4.0])
+    ok = _completing(make, starts, seeds, kw)
+    assert len(ok) >= 20
+    a, b = make(), make()
+    qa = a.run_RHMC_rj_batched([m.copy() for m, _ in ok], [s for _, s in ok], engine="native",
+                               **kw)
+    qb = b.run_RHMC_rj_batched([m.copy() for m, _ in ok], [s for _, s in ok], engine="python",
+                               **kw)
+    np.testing.assert_array_equal(a.move_chain, b.move_chain)
+    np.testing.assert_array_equal(a.N_chain, b.N_chain)
+    np.testing.assert_array_equal(a.A_chain, b.A_chain)
+    assert not a.flag_chain.any()
+    assert_state_close(a.q_chain, b.q_chain, 1e-11, "q_chain")
+    assert_state_close(a.p_chain, b.p_chain, 1e-11, "p_chain")
+    np.testing.assert_allclose(a.E_chain, b.E_chain, rtol=1e-12)
+    np.testing.assert_allclose(a.V_chain, b.V_chain, rtol=1e-12)
+    for x, y in zip(qa, qb):
+        assert x.size == y.size
+        np.testing.assert_allclose(x, y, rtol=1e-11, atol=1e-11)
+    assert a.g_ff2 == b.g_ff2
+    # every move type happened and some jumps were accepted
+    assert set(np.unique(a.move_chain)) >= {0, 1, 2, 3, 4}
+    assert (a.move_chain[a.A_chain] > 0).any()
+
+
+def test_native_dead_ends_on_the_engine(gpu_lib):
+    """One-star starts with deaths and merges proposed often: the native
+    driver rejects the dead ends (the reference raises) and keeps every chain
+    at 1 <= K <= N_max; its chains stay finite."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    starts = [z[name + "/q_model"][:1].copy() for _ in range(16)]
+    q = g.run_RHMC_rj_batched(starts, list(range(16)), f_pos=True, Niter=10, Nsteps=4,
+                              dt=0.05, N_max=4, P_move=[0.2, 0.4, 0.4])
+    assert g.flag_chain.any()
+    assert not g.A_chain[g.flag_chain.astype(bool)].any()
+    assert (g.N_chain >= 1).all() and (g.N_chain <= 4).all()
+    assert all(np.isfinite(x).all() and 3 <= x.size <= 12 for x in q)

@@ -199,10 +199,11 @@ def test_run_RHMC_reversible_jump_moves(gpu_lib, name):
     np.testing.assert_allclose(g.E_chain, z[name + "/E_chain"], rtol=1e-11)
 
 
-def test_run_RHMC_rj_batched_equals_single_runs(gpu_lib):
+@pytest.mark.parametrize("engine", ["native", "python"])
+def test_run_RHMC_rj_batched_equals_single_runs(gpu_lib, engine):
     """run_RHMC_rj_batched: chains at different, changing star counts, each on
     its own seeded stream, with every GPU phase batched over the chains
-    (grouped by K).  Chain 0 is the reference's rj_all run (its seed and
+    (grouped by K) — through librhmc_rj.so (native) and the NumPy loop.  Chain 0 is the reference's rj_all run (its seed and
     start) and reproduces the golden; the others equal one run_RHMC per seed
     (which test_run_RHMC_reversible_jump_moves pins to the reference)."""
     z = load_golden("rj")
@@ -235,7 +236,8 @@ def test_run_RHMC_rj_batched_equals_single_runs(gpu_lib):
     g.D = z[name + "/D"]
     np.random.seed(1)
     before = np.random.get_state()[1].copy()
-    q_end = g.run_RHMC_rj_batched([c[0].copy() for c in chains], [c[1] for c in chains], **kw)
+    q_end = g.run_RHMC_rj_batched([c[0].copy() for c in chains], [c[1] for c in chains],
+                                  engine=engine, **kw)
     assert np.array_equal(np.random.get_state()[1], before)   # the global stream is untouched
     assert len(q_end) == 4
     # chain 0: the reference's own run

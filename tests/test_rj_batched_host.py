@@ -57,7 +57,7 @@ def test_rj_batched_equals_per_seed_runs(P_move, capsys):
     g = _gym()
     np.random.seed(5)
     before = np.random.get_state()[1].copy()
-    q_end = g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, **kw)
+    q_end = g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, engine="python", **kw)
     assert np.array_equal(np.random.get_state()[1], before)
     for c, h in enumerate(singles):
         assert np.array_equal(g.move_chain[:, c], h.move_chain)

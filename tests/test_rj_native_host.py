@@ -1,0 +1,184 @@
+"""CPU tests of librhmc_rj.so (include/rhmc_rj.h), the native reversible-jump
+driver, without a GPU:
+
+* its NumPy-legacy stream replica against numpy.random.RandomState itself
+  (random_sample, randn, randint, beta incl. scipy.stats.beta.rvs,
+  standard_gamma, standard_exponential): bit-identical;
+* its orchestration against the Python multi_gym.run_RHMC_rj_batched, both
+  driven by the same deterministic stand-ins for the two engine calls
+  (test_rj_batched_host._fake_gpu): identical move types, star counts and
+  accept decisions, states and energies equal to within a few ulp (the
+  native kinetic energy takes C libm's log where NumPy may use its own SIMD
+  log: one-ulp differences, nothing else);
+* dead ends (no star left, nothing to merge), host-thread invariance and
+  argument errors.
+
+The physics is pinned on the GPU (tests/test_gpu_rj_native.py)."""
+import warnings
+
+import numpy as np
+import pytest
+
+from test_rj_batched_host import _gym
+
+STARTS = [np.array([[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.]]),
+          np.array([[18.3, 10.5, 12.2], [19.4, 20.0, 18.4]]),
+          np.array([[18., 10.2, 12.7], [19., 20.3, 18.1], [20., 15., 25.], [19.5, 8., 9.]]),
+          np.array([[18.5, 16., 16.], [19.5, 11., 14.]])]
+
+
+@pytest.fixture(scope="module")
+def rj():
+    from rhmc_amd import rj_native
+    return rj_native
+
+
+def test_exports_match_header(rj):
+    import os
+    import re
+    from conftest import ROOT
+    txt = open(os.path.join(ROOT, "include", "rhmc_rj.h")).read()
+    declared = sorted(set(re.findall(r"\b(rhmc_[a-z_]+)\s*\(", txt)))
+    assert sorted(rj.EXPORTS) == declared
+    assert all(hasattr(rj.lib(), s) for s in declared)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 77, 12345, 2 ** 32 - 1])
+def test_stream_replica_is_bit_identical(rj, seed):
+    n = 4000
+    r = np.random.RandomState(seed)
+    assert np.array_equal(r.random_sample(n), rj.np_draws(seed, "random_sample", n))
+    r = np.random.RandomState(seed)
+    assert np.array_equal(r.randn(n), rj.np_draws(seed, "randn", n))
+    for hi in (1, 2, 3, 51, 120, 1000, 2 ** 31 + 5):
+        r = np.random.RandomState(seed)
+        ref = [r.randint(0, hi, size=1)[0] for _ in range(200)]
+        assert np.array_equal(np.array(ref, float), rj.np_draws(seed, "randint", 200, a=hi)), hi
+    for a, b in ((2., 2.), (0.5, 0.7), (1., 1.), (0.3, 3.), (5., 1.5)):
+        r = np.random.RandomState(seed)
+        ref = [r.beta(a, b) for _ in range(300)]
+        assert np.array_equal(np.array(ref), rj.np_draws(seed, "beta", 300, a=a, b=b)), (a, b)
+    for s in (0.3, 1.0, 2.5):
+        r = np.random.RandomState(seed)
+        assert np.array_equal(r.standard_gamma(s, size=300),
+                              rj.np_draws(seed, "standard_gamma", 300, a=s)), s
+    r = np.random.RandomState(seed)
+    assert np.array_equal(r.standard_exponential(300),
+                          rj.np_draws(seed, "standard_exponential", 300))
+
+
+def test_scipy_beta_rvs_is_the_replica(rj):
+    """split_merge_move draws F with scipy.stats.beta.rvs on the global stream
+    (sampler_RHMC.py:1302): the legacy beta of the same stream."""
+    from scipy.stats import beta as BETA
+    np.random.seed(3)
+    np.random.randn(5)
+    a = BETA.rvs(2., 2., size=1)[0]
+    r = np.random.RandomState(3)
+    r.randn(5)
+    assert a == r.beta(2., 2.)
+
+
+def _native(rj, g, starts, seeds, kw, n_threads=4):
+    from rhmc_amd import capi
+    qms = [g.format_q(m.copy()) for m in starts]
+    P = g._params(for_energy=True)
+    fake_V, fake_S = g.V, g.RHMC_steps
+
+    def steps(q, p, ns):
+        qq, pp = fake_S(q, p, ns)
+        q[:] = qq
+        p[:] = pp
+    return rj.run(P, qms, seeds, kw["Niter"], kw["Nsteps"], kw["N_max"], kw["P_move"],
+                  capi.V_FLUX_WALL if kw["f_pos"] else 0, g.num_rows, g.num_cols, g.fmin, g.fmax,
+                  g.K_split, g.beta_a, g.beta_b, physics=(lambda q, fp: fake_V(q), steps),
+                  n_threads=n_threads)
+
+
+def _clean(g, N_max):
+    """Chains whose Python run never proposed a dead end (a death / merge at
+    one star, a birth / split at N_max): the reference raises there (and the
+    stand-ins would carry on with zero stars), the native driver rejects."""
+    mv, N = g.move_chain, g.N_chain
+    dead = ((np.isin(mv, (2, 4)) & (N <= 1)) | (np.isin(mv, (1, 3)) & (N >= N_max)))
+    return ~dead.any(axis=0)
+
+
+@pytest.mark.parametrize("P_move", [[0.4, 0.3, 0.3], [0.2, 0.8, 0.0], [0.2, 0.0, 0.8]])
+def test_native_equals_python_batched(rj, P_move):
+    starts = STARTS * 10
+    seeds = list(range(11, 11 + len(starts)))
+    kw = dict(f_pos=True, Niter=20, Nsteps=3, dt=0.05, N_max=12, P_move=P_move)
+    g = _gym()
+    with warnings.catch_warnings(), np.errstate(all="ignore"):
+        warnings.simplefilter("ignore")
+        ok = []
+        for m, s in zip(starts, seeds):      # chains whose Python run completes
+            try:
+                _gym().run_RHMC_rj_batched([m.copy()], [s], engine="python", **kw)
+                ok.append((m, s))
+            except ValueError:
+                pass
+        g.run_RHMC_rj_batched([m.copy() for m, _ in ok], [s for _, s in ok],
+                              engine="python", **kw)
+    assert len(ok) >= 5
+    h = _gym()
+    q_end, rec = _native(rj, h, [m for m, _ in ok], [s for _, s in ok], kw)
+    clean = _clean(g, kw["N_max"])
+    assert clean.sum() >= 4
+    np.testing.assert_array_equal(rec["move"][:, clean], g.move_chain[:, clean])
+    np.testing.assert_array_equal(rec["n_stars"][:, clean], g.N_chain[:, clean])
+    np.testing.assert_array_equal(rec["accept"][:, clean].astype(bool), g.A_chain[:, clean])
+    assert not rec["flags"][:, clean].any()
+    for k in ("q_chain", "p_chain", "E_chain", "V_chain", "T_chain"):
+        a, b = rec[k][:, clean], getattr(g, k)[:, clean]
+        np.testing.assert_allclose(a, b, rtol=1e-13, atol=1e-13, err_msg=k)
+    # the run really jumped
+    assert (g.move_chain[:, clean] > 0).any() and len(set(g.N_chain[:, clean].ravel())) > 1
+
+
+def test_dead_ends_are_rejected_and_threads_do_not_matter(rj):
+    """Deaths / merges at one star: the native driver rejects them (flag
+    DEAD_END, state back to the iteration's start, no accept draw) and every
+    chain's record is independent of the host thread count."""
+    starts = [np.array([[18.5, 16., 16.]])] * 20 + STARTS * 5
+    seeds = list(range(100, 100 + len(starts)))
+    kw = dict(f_pos=True, Niter=25, Nsteps=2, dt=0.05, N_max=6, P_move=[0.2, 0.4, 0.4])
+    _, r1 = _native(rj, _gym(), starts, seeds, kw, n_threads=1)
+    q4, r4 = _native(rj, _gym(), starts, seeds, kw, n_threads=7)
+    for k in r1:
+        assert np.array_equal(r1[k], r4[k]), k
+    fl = r1["flags"].astype(bool)
+    assert fl.any()
+    assert not r1["accept"][fl].any()
+    assert (r1["n_stars"] >= 1).all() and (r1["n_stars"] <= 6).all()
+    # a dead-end iteration leaves the chain where it started
+    l, c = np.argwhere(fl[:-1])[0]
+    assert r1["n_stars"][l + 1, c] == r1["n_stars"][l, c]
+    assert np.array_equal(r1["q_chain"][l + 1, c], r1["q_chain"][l, c])
+    assert all(q.size % 3 == 0 and 3 <= q.size <= 18 for q in q4)
+
+
+def test_argument_errors(rj):
+    from rhmc_amd import capi
+    g = _gym()
+    P = g._params(for_energy=True)
+    phys = (lambda q, fp: np.zeros(len(q)), lambda q, p, ns: None)
+    base = dict(n_iter=2, n_steps=1, N_max=4, P_move=[0.5, 0.25, 0.25], f_pos=1, rows=32,
+                cols=32, fmin=g.fmin, fmax=g.fmax, K_split=1., beta_a=2., beta_b=2.)
+    q = [g.format_q(STARTS[1].copy())]
+    with pytest.raises(capi.RhmcError, match="P_move"):
+        rj.run(P, q, [1], **dict(base, P_move=[0.5, 0.2, 0.2]), physics=phys)
+    with pytest.raises(capi.RhmcError, match="N_max"):
+        rj.run(P, q, [1], **dict(base, N_max=300), physics=phys)
+    with pytest.raises(capi.RhmcError, match="fmin"):
+        rj.run(P, q, [1], **dict(base, fmin=0.), physics=phys)
+    with pytest.raises(ValueError):
+        rj.run(P, [g.format_q(STARTS[2].copy())], [1], **dict(base, N_max=3), physics=phys)
+    with pytest.raises(ValueError, match="seeds"):
+        rj.run(P, q, [-1], **base, physics=phys)
+    # an engine failure surfaces as the engine's error
+    with pytest.raises(RuntimeError, match="boom"):
+        def bad(q, fp):
+            raise RuntimeError("boom")
+        rj.run(P, q, [1], **base, physics=(bad, phys[1]))
