@@ -28,6 +28,8 @@
 #include <thread>
 #include <vector>
 
+#include <hip/hip_runtime_api.h>
+
 #include "np_legacy.hpp"
 
 namespace {
@@ -170,7 +172,14 @@ struct Run {
     return 0;
   }
 
+  // optional: every group's trajectory in one call (the context path: the
+  // groups run concurrently on several HIP streams)
+  int (*steps_groups)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
+                      const int64_t* n, double* const* q, double* const* p,
+                      int32_t n_steps) = nullptr;
+
   int trajectories(const std::vector<int64_t>& idx) {
+    if (steps_groups) return trajectories_grouped(idx);
     std::vector<double> qb, pb;
     for (auto& grp : groups(idx)) {
       const int32_t K = grp.first;
@@ -188,6 +197,42 @@ struct Run {
       for (size_t i = 0; i < cs.size(); ++i) {
         std::memcpy(ch[cs[i]].q.data(), &qb[i * d], d * 8);
         std::memcpy(ch[cs[i]].p.data(), &pb[i * d], d * 8);
+      }
+    }
+    return 0;
+  }
+
+  int trajectories_grouped(const std::vector<int64_t>& idx) {
+    const auto gs = groups(idx);
+    if (gs.empty()) return 0;
+    const int32_t G = (int32_t)gs.size();
+    std::vector<std::vector<double>> qb((size_t)G), pb((size_t)G);
+    std::vector<int32_t> Ks((size_t)G);
+    std::vector<int64_t> ns((size_t)G);
+    std::vector<double*> qp((size_t)G), pp((size_t)G);
+    for (int32_t g = 0; g < G; ++g) {
+      const auto& cs = gs[g].second;
+      const size_t d = 3 * (size_t)gs[g].first;
+      Ks[g] = gs[g].first;
+      ns[g] = (int64_t)cs.size();
+      qb[g].resize(cs.size() * d);
+      pb[g].resize(cs.size() * d);
+      for (size_t i = 0; i < cs.size(); ++i) {
+        std::memcpy(&qb[g][i * d], ch[cs[i]].q.data(), d * 8);
+        std::memcpy(&pb[g][i * d], ch[cs[i]].p.data(), d * 8);
+      }
+      qp[g] = qb[g].data();
+      pp[g] = pb[g].data();
+    }
+    const int rc = steps_groups(phys->user, &P, G, Ks.data(), ns.data(), qp.data(), pp.data(),
+                                cfg->n_steps);
+    if (rc != 0) return engine_fail(rc, "steps");
+    for (int32_t g = 0; g < G; ++g) {
+      const auto& cs = gs[g].second;
+      const size_t d = 3 * (size_t)gs[g].first;
+      for (size_t i = 0; i < cs.size(); ++i) {
+        std::memcpy(ch[cs[i]].q.data(), &qb[g][i * d], d * 8);
+        std::memcpy(ch[cs[i]].p.data(), &pb[g][i * d], d * 8);
       }
     }
     return 0;
@@ -355,12 +400,17 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
   return 0;
 }
 
-int run(const rhmc_rj_physics* phys, const rhmc_params* P0, const rhmc_rj_config* cfg,
-        double* q, int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
+using StepsGroups = int (*)(void*, const rhmc_params*, int32_t, const int32_t*,
+                           const int64_t*, double* const*, double* const*, int32_t);
+
+int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params* P0,
+        const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
+        const rhmc_rj_record* rec) {
   if (int rc = check(P0, cfg, q, K, seeds, n)) return rc;
   if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
   Run R;
   R.phys = phys;
+  R.steps_groups = steps_groups;
   R.P = *P0;
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
@@ -493,14 +543,101 @@ int run(const rhmc_rj_physics* phys, const rhmc_params* P0, const rhmc_rj_config
   return 0;
 }
 
-// the engine as physics
+// the engine as physics: V by rhmc_energy; the trajectories of all star-count
+// groups of a phase at once, each group on one of kStreams HIP streams
+// (rhmc_leapfrog_device), so that small groups fill the GPU together instead
+// of one after the other
+constexpr int kStreams = 4;
+
+struct CtxEngine {
+  rhmc_ctx* ctx = nullptr;
+  hipStream_t s[kStreams] = {};
+  double* d = nullptr;
+  size_t d_bytes = 0;
+  double* h = nullptr;
+  size_t h_bytes = 0;
+  ~CtxEngine() {
+    if (d) (void)hipFree(d);
+    if (h) (void)hipHostFree(h);
+    for (auto& st : s)
+      if (st) (void)hipStreamDestroy(st);
+  }
+};
+
+#define RJ_HIP(expr)                                                                   \
+  do {                                                                                 \
+    const hipError_t e_ = (expr);                                                      \
+    if (e_ != hipSuccess) return fail(RHMC_ERR_HIP, std::string(#expr) + ": " +        \
+                                                        hipGetErrorString(e_));        \
+  } while (0)
+
+int engine_init(CtxEngine& E) {
+  const double* dimg = nullptr;
+  if (int rc = rhmc_ctx_image_device(E.ctx, &dimg)) return rc;
+  if (!dimg) return fail(RHMC_ERR_ARG, "context has no image");
+  hipPointerAttribute_t at;
+  RJ_HIP(hipPointerGetAttributes(&at, dimg));
+  RJ_HIP(hipSetDevice(at.device));
+  for (auto& st : E.s) RJ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  return 0;
+}
+
 int ctx_energy(void* user, const rhmc_params* P, const double* q, int64_t n, int32_t K,
                int32_t f_pos, double* V) {
-  return rhmc_energy(static_cast<rhmc_ctx*>(user), P, q, nullptr, V, nullptr, n, K, f_pos);
+  return rhmc_energy(static_cast<CtxEngine*>(user)->ctx, P, q, nullptr, V, nullptr, n, K, f_pos);
 }
 int ctx_steps(void* user, const rhmc_params* P, double* q, double* p, int64_t n, int32_t K,
               int32_t n_steps) {
-  return rhmc_leapfrog(static_cast<rhmc_ctx*>(user), P, q, p, n, K, n_steps, nullptr, nullptr);
+  return rhmc_leapfrog(static_cast<CtxEngine*>(user)->ctx, P, q, p, n, K, n_steps, nullptr,
+                       nullptr);
+}
+int ctx_steps_groups(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
+                     const int64_t* n, double* const* q, double* const* p, int32_t n_steps) {
+  CtxEngine& E = *static_cast<CtxEngine*>(user);
+  std::vector<size_t> off((size_t)G), sb((size_t)G);
+  size_t total = 0;
+  for (int32_t g = 0; g < G; ++g) {
+    off[g] = total;
+    sb[g] = (size_t)n[g] * 3 * (size_t)K[g];  // doubles per q (and per p)
+    total += 2 * sb[g];
+  }
+  if (total * 8 > E.d_bytes) {
+    if (E.d) RJ_HIP(hipFree(E.d));
+    E.d = nullptr;
+    E.d_bytes = 0;
+    RJ_HIP(hipMalloc(&E.d, total * 8));
+    E.d_bytes = total * 8;
+  }
+  if (total * 8 > E.h_bytes) {
+    if (E.h) RJ_HIP(hipHostFree(E.h));
+    E.h = nullptr;
+    E.h_bytes = 0;
+    RJ_HIP(hipHostMalloc(&E.h, total * 8, hipHostMallocDefault));
+    E.h_bytes = total * 8;
+  }
+  std::vector<int32_t> order((size_t)G);
+  for (int32_t g = 0; g < G; ++g) order[g] = g;
+  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return sb[a] > sb[b]; });
+  int rc = 0;
+  for (int32_t i = 0; i < G && rc == 0; ++i) {
+    const int32_t g = order[i];
+    hipStream_t st = E.s[i % kStreams];
+    double* hq = E.h + off[g];
+    double* dq = E.d + off[g];
+    std::memcpy(hq, q[g], sb[g] * 8);
+    std::memcpy(hq + sb[g], p[g], sb[g] * 8);
+    RJ_HIP(hipMemcpyAsync(dq, hq, 2 * sb[g] * 8, hipMemcpyHostToDevice, st));
+    rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb[g], n[g], K[g], n_steps, nullptr, nullptr,
+                              st);
+    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq, dq, 2 * sb[g] * 8, hipMemcpyDeviceToHost, st));
+  }
+  for (auto& st : E.s) RJ_HIP(hipStreamSynchronize(st));
+  if (rc) return rc;
+  for (int32_t g = 0; g < G; ++g) {
+    std::memcpy(q[g], E.h + off[g], sb[g] * 8);
+    std::memcpy(p[g], E.h + off[g] + sb[g], sb[g] * 8);
+  }
+  return 0;
 }
 
 }  // namespace
@@ -511,7 +648,7 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
                         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds,
                         int64_t n, const rhmc_rj_record* rec) {
   try {
-    return run(phys, P, cfg, q, K, seeds, n, rec);
+    return run(phys, nullptr, P, cfg, q, K, seeds, n, rec);
   } catch (const std::exception& e) {
     return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
   }
@@ -520,8 +657,16 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
 int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, double* q,
                 int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
-  rhmc_rj_physics phys{ctx, ctx_energy, ctx_steps};
-  return rhmc_rj_run_physics(&phys, P, cfg, q, K, seeds, n, rec);
+  try {
+    CtxEngine E;
+    E.ctx = ctx;
+    if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
+    if (int rc = engine_init(E)) return rc;
+    rhmc_rj_physics phys{&E, ctx_energy, ctx_steps};
+    return run(&phys, ctx_steps_groups, P, cfg, q, K, seeds, n, rec);
+  } catch (const std::exception& e) {
+    return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
+  }
 }
 
 int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, double* out) {
