@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -429,6 +430,13 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
   }
   const int64_t rows_n = (int64_t)cfg->n_iter + 1;
   std::vector<double> V0((size_t)n), V1((size_t)n), T0((size_t)n);
+  double phase[7] = {0, 0, 0, 0, 0, 0, 0};
+  auto clk = std::chrono::steady_clock::now();
+  auto lap = [&](int i) {  // the time since the last lap goes to phase i
+    const auto t = std::chrono::steady_clock::now();
+    phase[i] += std::chrono::duration<double>(t - clk).count();
+    clk = t;
+  };
   for (int64_t l = 0; l < rows_n; ++l) {
     if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
     if (cfg->n_beta > 0) R.P.beta = cfg->schedule_beta[std::min<int64_t>(l, cfg->n_beta - 1)];
@@ -452,6 +460,7 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
       h.K0 = h.K;
       h.dead = false;
     });
+    lap(0);
     // 2. V(q)
     if (int rc = R.energies(all, V0)) return rc;
     R.parallel(all, [&](int64_t c) {
@@ -477,8 +486,10 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
           rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
       }
     });
+    lap(1);
     // 3. the trajectory of every chain
     if (int rc = R.trajectories(all)) return rc;
+    lap(2);
     // 4. the proposals
     std::vector<int64_t> jump;
     for (int64_t c = 0; c < n; ++c)
@@ -496,8 +507,10 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
     std::vector<int64_t> live;
     for (int64_t c : jump)
       if (!R.ch[c].dead) live.push_back(c);
+    lap(3);
     // 5. the trajectory after the jump
     if (int rc = R.trajectories(live)) return rc;
+    lap(4);
     for (int64_t c : live)
       for (auto& v : R.ch[c].p) v = -v;
     // 6. V(q')
@@ -505,6 +518,7 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
     for (int64_t c = 0; c < n; ++c)
       if (!R.ch[c].dead) scored.push_back(c);
     if (int rc = R.energies(scored, V1)) return rc;
+    lap(5);
     // 7. accept / reject
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
@@ -533,7 +547,10 @@ int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params
         if (rec->flags) rec->flags[r] = h.dead ? (int32_t)RHMC_RJ_DEAD_END : 0;
       }
     });
+    lap(6);
   }
+  if (rec && rec->phase_s)
+    for (int i = 0; i < 7; ++i) rec->phase_s[i] = phase[i];
   for (int64_t c = 0; c < n; ++c) {
     const Chain& h = R.ch[c];
     std::fill(q + c * W, q + (c + 1) * W, 0.);

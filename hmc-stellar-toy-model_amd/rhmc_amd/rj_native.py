@@ -46,7 +46,8 @@ class RjConfig(ctypes.Structure):
 class RjRecord(ctypes.Structure):
     """Mirror of `rhmc_rj_record`."""
     _fields_ = [(n, ctypes.c_void_p) for n in ("q_chain", "p_chain", "E_chain", "V_chain",
-                                                "T_chain", "accept", "move", "n_stars", "flags")]
+                                                "T_chain", "accept", "move", "n_stars", "flags",
+                                                "phase_s")]
 
 
 def _load():
@@ -138,10 +139,10 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
            "E_chain": np.zeros((rows_n, n)), "V_chain": np.zeros((rows_n, n)),
            "T_chain": np.zeros((rows_n, n)), "accept": np.zeros((rows_n, n), np.int32),
            "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),
-           "flags": np.zeros((rows_n, n), np.int32)}
+           "flags": np.zeros((rows_n, n), np.int32), "phase_s": np.zeros(7)}
     r = RjRecord(*[rec[k].ctypes.data for k in ("q_chain", "p_chain", "E_chain", "V_chain",
                                                   "T_chain", "accept", "move", "n_stars",
-                                                  "flags")])
+                                                  "flags", "phase_s")])
     if ctx is not None:
         _check(_lib.rhmc_rj_run(ctx._h, ctypes.byref(params), ctypes.byref(cfg), q.ctypes.data,
                                 K.ctypes.data, sd.ctypes.data, n, ctypes.byref(r)))

@@ -838,6 +838,8 @@ class multi_gym(base_class):
         self.move_chain = rec["move"].astype(int)
         self.N_chain = rec["n_stars"].astype(int)
         self.flag_chain = rec["flags"]
+        self.rj_phase_s = dict(zip(("draws", "V0", "steps1", "proposals", "steps2", "V1",
+                                    "accept"), rec["phase_s"]))
         self.Nobjs = self.d = None
         return q_end
 

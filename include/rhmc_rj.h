@@ -92,6 +92,10 @@ typedef struct rhmc_rj_record {
   int32_t* move;     /* 0 within, 1 birth, 2 death, 3 split, 4 merge      */
   int32_t* n_stars;  /* N_chain                                           */
   int32_t* flags;    /* RHMC_RJ_* bits of the iteration                   */
+  double* phase_s;   /* [7] wall seconds summed over the run: momentum +
+                        move draws (host), V(q), first trajectories,
+                        proposals (host), second trajectories, V(q'),
+                        accept (host)                                     */
 } rhmc_rj_record;
 
 #define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */

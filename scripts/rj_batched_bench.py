@@ -41,7 +41,7 @@ def main():
     starts = []
     for c in range(args.chains):
         q = wl.q0[c].reshape(-1, 3).copy()
-        q[:, 0] = g.flux2mag_converter(q[:, 0])
+        q[:, 0] = np.minimum(g.flux2mag_converter(q[:, 0]), 22.5)   # above the flux wall
         starts.append(q)
     gpu = {"s": 0.0, "calls": 0}
     for name in (("V", "RHMC_steps") if args.engine == "python" else ()):  # time GPU calls
@@ -75,7 +75,9 @@ def main():
            "gpu_call_share": gpu["s"] / wall if args.engine == "python" else None,
            "gpu_calls": gpu["calls"] if args.engine == "python" else None,
            "accepted_jumps": int(np.sum(g.A_chain & (moves > 0))),
-           "star_count_range_end": [int(g.N_chain[-1].min()), int(g.N_chain[-1].max())]}
+           "star_count_range_end": [int(g.N_chain[-1].min()), int(g.N_chain[-1].max())],
+           "distinct_star_counts": int(len(np.unique(g.N_chain))),
+           "phase_s": getattr(g, "rj_phase_s", None) if args.engine == "native" else None}
     print(json.dumps(out))
 
 

@@ -147,7 +147,9 @@ def test_dead_ends_are_rejected_and_threads_do_not_matter(rj):
     _, r1 = _native(rj, _gym(), starts, seeds, kw, n_threads=1)
     q4, r4 = _native(rj, _gym(), starts, seeds, kw, n_threads=7)
     for k in r1:
-        assert np.array_equal(r1[k], r4[k]), k
+        if k != "phase_s":                            # wall times
+            assert np.array_equal(r1[k], r4[k]), k
+    assert (r1["phase_s"] >= 0).all() and r1["phase_s"].sum() > 0
     fl = r1["flags"].astype(bool)
     assert fl.any()
     assert not r1["accept"][fl].any()
