@@ -85,17 +85,37 @@ int64_t choice(rhmc_np::Legacy& r, const double* w, int64_t k, std::vector<doubl
   return std::upper_bound(cdf.begin(), cdf.end(), u) - cdf.begin();
 }
 
-// scipy.stats.beta.logpdf / pdf (xlog1py(b-1, -x) + xlogy(a-1, x) - betaln(a, b))
-double beta_logpdf(double x, double a, double b) {
-  const double lb = std::lgamma(a) + std::lgamma(b) - std::lgamma(a + b);
-  const double t1 = (b - 1.0 == 0.0) ? 0.0 : (b - 1.0) * std::log1p(-x);
-  const double t2 = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * std::log(x);
-  return t1 + t2 - lb;
-}
-double beta_pdf(double x, double a, double b) {
-  if (!(x >= 0.0 && x <= 1.0)) return 0.0;
-  return std::exp(beta_logpdf(x, a, b));
-}
+// scipy.stats.beta.logpdf / pdf: xlog1py(b-1, -x) + xlogy(a-1, x) - betaln(a, b);
+// the pdf with integer exponents as products (the merge evaluates it on every
+// star pair: beta_a = beta_b = 2 by default, 6 x (1 - x))
+struct BetaDist {
+  double a = 2., b = 2., lb = 0., inv_b = 0.;
+  int ia = -1, ib = -1;  // a - 1, b - 1 when small non-negative integers
+  void set(double a_, double b_) {
+    a = a_;
+    b = b_;
+    lb = std::lgamma(a) + std::lgamma(b) - std::lgamma(a + b);
+    inv_b = std::exp(-lb);
+    ia = (a - 1 >= 0 && a - 1 <= 8 && a == std::floor(a)) ? (int)(a - 1) : -1;
+    ib = (b - 1 >= 0 && b - 1 <= 8 && b == std::floor(b)) ? (int)(b - 1) : -1;
+  }
+  double logpdf(double x) const {
+    const double t1 = (b - 1.0 == 0.0) ? 0.0 : (b - 1.0) * std::log1p(-x);
+    const double t2 = (a - 1.0 == 0.0) ? 0.0 : (a - 1.0) * std::log(x);
+    return t1 + t2 - lb;
+  }
+  double pdf(double x) const {
+    if (!(x >= 0.0 && x <= 1.0)) return 0.0;
+    if (ia >= 0 && ib >= 0) {
+      double v = inv_b;
+      for (int k = 0; k < ia; ++k) v *= x;
+      const double y = 1.0 - x;
+      for (int k = 0; k < ib; ++k) v *= y;
+      return v;
+    }
+    return std::exp(logpdf(x));
+  }
+};
 
 // ------------------------------------------------------------------- chains
 struct Chain {
@@ -115,6 +135,7 @@ struct Run {
   std::vector<Chain> ch;
   int nt;
   int Kmax;
+  BetaDist beta;
 
   template <class F>
   void parallel(const std::vector<int64_t>& idx, F f) {
@@ -173,14 +194,20 @@ struct Run {
     return 0;
   }
 
-  // optional: every group's trajectory in one call (the context path: the
-  // groups run concurrently on several HIP streams)
-  int (*steps_groups)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
-                      const int64_t* n, double* const* q, double* const* p,
-                      int32_t n_steps) = nullptr;
+  // optional (the context path): a phase's groups staged in one pinned buffer
+  // and run concurrently on several HIP streams.  buffer(user, doubles)
+  // returns the staging area; launch(...) runs group g from q at off[g] and
+  // p at off[g] + n[g] 3 K[g], in place.
+  struct Staged {
+    void* user = nullptr;
+    double* (*buffer)(void* user, size_t doubles) = nullptr;
+    int (*launch)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
+                  const int64_t* n, const size_t* off, int32_t n_steps) = nullptr;
+  };
+  Staged staged;
 
   int trajectories(const std::vector<int64_t>& idx) {
-    if (steps_groups) return trajectories_grouped(idx);
+    if (staged.launch) return trajectories_staged(idx);
     std::vector<double> qb, pb;
     for (auto& grp : groups(idx)) {
       const int32_t K = grp.first;
@@ -203,39 +230,49 @@ struct Run {
     return 0;
   }
 
-  int trajectories_grouped(const std::vector<int64_t>& idx) {
+  int trajectories_staged(const std::vector<int64_t>& idx) {
     const auto gs = groups(idx);
     if (gs.empty()) return 0;
     const int32_t G = (int32_t)gs.size();
-    std::vector<std::vector<double>> qb((size_t)G), pb((size_t)G);
     std::vector<int32_t> Ks((size_t)G);
     std::vector<int64_t> ns((size_t)G);
-    std::vector<double*> qp((size_t)G), pp((size_t)G);
+    std::vector<size_t> off((size_t)G);
+    size_t total = 0;
     for (int32_t g = 0; g < G; ++g) {
-      const auto& cs = gs[g].second;
-      const size_t d = 3 * (size_t)gs[g].first;
       Ks[g] = gs[g].first;
-      ns[g] = (int64_t)cs.size();
-      qb[g].resize(cs.size() * d);
-      pb[g].resize(cs.size() * d);
-      for (size_t i = 0; i < cs.size(); ++i) {
-        std::memcpy(&qb[g][i * d], ch[cs[i]].q.data(), d * 8);
-        std::memcpy(&pb[g][i * d], ch[cs[i]].p.data(), d * 8);
-      }
-      qp[g] = qb[g].data();
-      pp[g] = pb[g].data();
+      ns[g] = (int64_t)gs[g].second.size();
+      off[g] = total;
+      total += 2 * (size_t)ns[g] * 3 * (size_t)Ks[g];
     }
-    const int rc = steps_groups(phys->user, &P, G, Ks.data(), ns.data(), qp.data(), pp.data(),
-                                cfg->n_steps);
-    if (rc != 0) return engine_fail(rc, "steps");
+    double* h = staged.buffer(staged.user, total);
+    if (!h) return fail(RHMC_ERR_NOMEM, "staging buffer: " + g_err);
+    // slot j of the phase: its chain, its q row and the offset of its p row
+    // (group g's p block follows its q block) in the staging buffer
+    std::vector<int64_t> slots, slot_c;
+    std::vector<double*> slot_q;
+    std::vector<size_t> pofs;
     for (int32_t g = 0; g < G; ++g) {
-      const auto& cs = gs[g].second;
-      const size_t d = 3 * (size_t)gs[g].first;
-      for (size_t i = 0; i < cs.size(); ++i) {
-        std::memcpy(ch[cs[i]].q.data(), &qb[g][i * d], d * 8);
-        std::memcpy(ch[cs[i]].p.data(), &pb[g][i * d], d * 8);
+      const size_t d = 3 * (size_t)Ks[g];
+      for (size_t i = 0; i < gs[g].second.size(); ++i) {
+        slots.push_back((int64_t)slots.size());
+        slot_c.push_back(gs[g].second[i]);
+        slot_q.push_back(h + off[g] + i * d);
+        pofs.push_back((size_t)ns[g] * d);
       }
     }
+    parallel(slots, [&](int64_t j) {
+      const Chain& c = ch[slot_c[j]];
+      std::memcpy(slot_q[j], c.q.data(), c.q.size() * 8);
+      std::memcpy(slot_q[j] + pofs[j], c.p.data(), c.p.size() * 8);
+    });
+    const int rc = staged.launch(staged.user, &P, G, Ks.data(), ns.data(), off.data(),
+                                 cfg->n_steps);
+    if (rc != 0) return engine_fail(rc, "steps");
+    parallel(slots, [&](int64_t j) {
+      Chain& c = ch[slot_c[j]];
+      std::memcpy(c.q.data(), slot_q[j], c.q.size() * 8);
+      std::memcpy(c.p.data(), slot_q[j] + pofs[j], c.p.size() * 8);
+    });
     return 0;
   }
 
@@ -307,7 +344,7 @@ struct Run {
       M.star(qs[0], Hs);
       const double Ts = kinetic(ps, Hs, 3, c.tmp);
       const double T1 = kinetic(p1, H1, 3, c.tmp), T2 = kinetic(p2, H2, 3, c.tmp);
-      c.factor = (-3 / 2.) + std::log(fs) - beta_logpdf(F, a, b) + ln_q_dxdy + (dr_sq / two_ks2) +
+      c.factor = (-3 / 2.) + std::log(fs) - beta.logpdf(F) + ln_q_dxdy + (dr_sq / two_ks2) +
                  T1 + T2 - Ts;
       for (int t = 0; t < 3; ++t) {
         c.q[3 * i + t] = q1[t];
@@ -326,11 +363,11 @@ struct Run {
       for (int64_t s = 0; s < n; ++s) {
         const double fr = c.q[3 * r], fc = c.q[3 * s];
         const double Fm = fc / (fr + fc);
-        double v = beta_pdf(Fm, a, b);
+        double v = beta.pdf(Fm);
         if (std::fabs(Fm - 0.5) < 1e-6) v = 0.;
         const double ddx = c.q[3 * r + 1] - c.q[3 * s + 1], ddy = c.q[3 * r + 2] - c.q[3 * s + 2];
         const double Rsq = std::pow(ddx, 2) + std::pow(ddy, 2);
-        P2[r * n + s] = v * (std::exp(-Rsq / (2. * std::pow(Ks, 2))) / (2. * kPi * std::pow(Ks, 2)));
+        P2[r * n + s] = v * (std::exp(-Rsq / two_ks2) / two_pi_ks2);
       }
     const double tot = rhmc_np::pairwise_sum(P2.data(), n * n);
     if (!(tot > 0.0) || !std::isfinite(tot)) return false;  // the reference raises here
@@ -365,7 +402,7 @@ struct Run {
     }
     nq.insert(nq.end(), qs, qs + 3);
     np_.insert(np_.end(), ps, ps + 3);
-    c.factor = (3 / 2.) - std::log(qs[0]) + beta_logpdf(F, a, b) - ln_q_dxdy - (dr_sq / two_ks2) -
+    c.factor = (3 / 2.) - std::log(qs[0]) + beta.logpdf(F) - ln_q_dxdy - (dr_sq / two_ks2) -
                T1 - T2 + Ts;
     c.q.swap(nq);
     c.p.swap(np_);
@@ -401,20 +438,18 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
   return 0;
 }
 
-using StepsGroups = int (*)(void*, const rhmc_params*, int32_t, const int32_t*,
-                           const int64_t*, double* const*, double* const*, int32_t);
-
-int run(const rhmc_rj_physics* phys, StepsGroups steps_groups, const rhmc_params* P0,
+int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_params* P0,
         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
         const rhmc_rj_record* rec) {
   if (int rc = check(P0, cfg, q, K, seeds, n)) return rc;
   if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
   Run R;
   R.phys = phys;
-  R.steps_groups = steps_groups;
+  if (staged) R.staged = *staged;
   R.P = *P0;
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
+  R.beta.set(cfg->beta_a, cfg->beta_b);
   int nt = cfg->n_threads;
   if (nt <= 0) nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
   R.nt = nt;
@@ -608,53 +643,52 @@ int ctx_steps(void* user, const rhmc_params* P, double* q, double* p, int64_t n,
   return rhmc_leapfrog(static_cast<CtxEngine*>(user)->ctx, P, q, p, n, K, n_steps, nullptr,
                        nullptr);
 }
-int ctx_steps_groups(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
-                     const int64_t* n, double* const* q, double* const* p, int32_t n_steps) {
+double* ctx_buffer(void* user, size_t doubles) {
   CtxEngine& E = *static_cast<CtxEngine*>(user);
-  std::vector<size_t> off((size_t)G), sb((size_t)G);
-  size_t total = 0;
-  for (int32_t g = 0; g < G; ++g) {
-    off[g] = total;
-    sb[g] = (size_t)n[g] * 3 * (size_t)K[g];  // doubles per q (and per p)
-    total += 2 * sb[g];
-  }
-  if (total * 8 > E.d_bytes) {
-    if (E.d) RJ_HIP(hipFree(E.d));
+  const size_t bytes = doubles * 8;
+  if (bytes > E.d_bytes) {
+    if (E.d) (void)hipFree(E.d);
     E.d = nullptr;
     E.d_bytes = 0;
-    RJ_HIP(hipMalloc(&E.d, total * 8));
-    E.d_bytes = total * 8;
+    if (hipMalloc(&E.d, bytes) != hipSuccess) {
+      g_err = "hipMalloc failed";
+      return nullptr;
+    }
+    E.d_bytes = bytes;
   }
-  if (total * 8 > E.h_bytes) {
-    if (E.h) RJ_HIP(hipHostFree(E.h));
+  if (bytes > E.h_bytes) {
+    if (E.h) (void)hipHostFree(E.h);
     E.h = nullptr;
     E.h_bytes = 0;
-    RJ_HIP(hipHostMalloc(&E.h, total * 8, hipHostMallocDefault));
-    E.h_bytes = total * 8;
+    if (hipHostMalloc(&E.h, bytes, hipHostMallocDefault) != hipSuccess) {
+      g_err = "hipHostMalloc failed";
+      return nullptr;
+    }
+    E.h_bytes = bytes;
   }
+  return E.h;
+}
+
+int ctx_launch(void* user, const rhmc_params* P, int32_t G, const int32_t* K, const int64_t* n,
+               const size_t* off, int32_t n_steps) {
+  CtxEngine& E = *static_cast<CtxEngine*>(user);
   std::vector<int32_t> order((size_t)G);
   for (int32_t g = 0; g < G; ++g) order[g] = g;
-  std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return sb[a] > sb[b]; });
+  std::stable_sort(order.begin(), order.end(),
+                   [&](int32_t a, int32_t b) { return n[a] * K[a] > n[b] * K[b]; });
   int rc = 0;
-  for (int32_t i = 0; i < G && rc == 0; ++i) {
+  for (int32_t i = 0; i < G && rc == 0; ++i) {  // largest groups first
     const int32_t g = order[i];
+    const size_t sb = (size_t)n[g] * 3 * (size_t)K[g];
     hipStream_t st = E.s[i % kStreams];
     double* hq = E.h + off[g];
     double* dq = E.d + off[g];
-    std::memcpy(hq, q[g], sb[g] * 8);
-    std::memcpy(hq + sb[g], p[g], sb[g] * 8);
-    RJ_HIP(hipMemcpyAsync(dq, hq, 2 * sb[g] * 8, hipMemcpyHostToDevice, st));
-    rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb[g], n[g], K[g], n_steps, nullptr, nullptr,
-                              st);
-    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq, dq, 2 * sb[g] * 8, hipMemcpyDeviceToHost, st));
+    RJ_HIP(hipMemcpyAsync(dq, hq, 2 * sb * 8, hipMemcpyHostToDevice, st));
+    rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb, n[g], K[g], n_steps, nullptr, nullptr, st);
+    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq, dq, 2 * sb * 8, hipMemcpyDeviceToHost, st));
   }
   for (auto& st : E.s) RJ_HIP(hipStreamSynchronize(st));
-  if (rc) return rc;
-  for (int32_t g = 0; g < G; ++g) {
-    std::memcpy(q[g], E.h + off[g], sb[g] * 8);
-    std::memcpy(p[g], E.h + off[g] + sb[g], sb[g] * 8);
-  }
-  return 0;
+  return rc;
 }
 
 }  // namespace
@@ -680,7 +714,11 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
     if (int rc = engine_init(E)) return rc;
     rhmc_rj_physics phys{&E, ctx_energy, ctx_steps};
-    return run(&phys, ctx_steps_groups, P, cfg, q, K, seeds, n, rec);
+    Run::Staged st;
+    st.user = &E;
+    st.buffer = ctx_buffer;
+    st.launch = ctx_launch;
+    return run(&phys, &st, P, cfg, q, K, seeds, n, rec);
   } catch (const std::exception& e) {
     return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
   }

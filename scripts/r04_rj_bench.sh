@@ -1,0 +1,20 @@
+#!/bin/bash
+# Native vs NumPy-loop reversible-jump throughput at big-sim4 geometry, with
+# the native driver's per-phase wall times.  Logs under gpurun_out/r04_rj/.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+O=gpurun_out/r04_rj
+mkdir -p $O
+export TMPDIR=/tmp
+step() {
+  local lim=$1 name=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$O/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; grep chain_leap "$O/$name.log" | tail -1
+  if [ $rc -ne 0 ]; then tail -5 "$O/$name.log"; exit $rc; fi
+}
+for n in 256 1024 4096 16384; do
+  step 300 native_$n python3 -u scripts/rj_batched_bench.py --engine native --chains $n --niter 10 --nsteps 20
+done
+step 300 python_256 python3 -u scripts/rj_batched_bench.py --engine python --chains 256 --niter 10 --nsteps 20
+step 300 native_4096_t1 python3 -u scripts/rj_batched_bench.py --engine native --chains 4096 --niter 10 --nsteps 20 --threads 1
+echo done
