@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -601,6 +602,18 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
 // of one after the other
 constexpr int kStreams = 4;
 
+// The streams live for the process, kStreams per device, created on first use
+// and warmed by one small copy each: the first dispatch to a new HIP stream
+// binds its hardware queue, which cost 6-11 ms per stream when it happened
+// inside a run (profiles/r04_rj/).
+struct DeviceStreams {
+  hipStream_t s[kStreams] = {};
+  double* warm = nullptr;
+};
+
+std::mutex g_streams_mu;
+std::map<int, DeviceStreams> g_streams;
+
 struct CtxEngine {
   rhmc_ctx* ctx = nullptr;
   hipStream_t s[kStreams] = {};
@@ -611,8 +624,6 @@ struct CtxEngine {
   ~CtxEngine() {
     if (d) (void)hipFree(d);
     if (h) (void)hipHostFree(h);
-    for (auto& st : s)
-      if (st) (void)hipStreamDestroy(st);
   }
 };
 
@@ -630,7 +641,17 @@ int engine_init(CtxEngine& E) {
   hipPointerAttribute_t at;
   RJ_HIP(hipPointerGetAttributes(&at, dimg));
   RJ_HIP(hipSetDevice(at.device));
-  for (auto& st : E.s) RJ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  std::lock_guard<std::mutex> lock(g_streams_mu);
+  DeviceStreams& ds = g_streams[at.device];
+  if (!ds.warm) {
+    RJ_HIP(hipMalloc(&ds.warm, kStreams * sizeof(double)));
+    for (int i = 0; i < kStreams; ++i) {
+      RJ_HIP(hipStreamCreateWithFlags(&ds.s[i], hipStreamNonBlocking));
+      RJ_HIP(hipMemsetAsync(ds.warm + i, 0, sizeof(double), ds.s[i]));
+    }
+    for (int i = 0; i < kStreams; ++i) RJ_HIP(hipStreamSynchronize(ds.s[i]));
+  }
+  for (int i = 0; i < kStreams; ++i) E.s[i] = ds.s[i];
   return 0;
 }
 
