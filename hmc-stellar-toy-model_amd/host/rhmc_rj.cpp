@@ -22,6 +22,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -118,6 +120,74 @@ struct BetaDist {
   }
 };
 
+// ------------------------------------------------------------- thread pool
+// Fork-join pool that lives for one run: the workers sleep between phases
+// (spawning threads per phase cost ~3 ms per iteration at 16 threads).
+class Pool {
+ public:
+  explicit Pool(int n) {
+    for (int t = 1; t < n; ++t) th_.emplace_back([this] { worker(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  int size() const { return (int)th_.size() + 1; }
+  // body(i) for i in [0, n), chunks of 16, the caller works too
+  void run(int64_t n, const std::function<void(int64_t)>& body) {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      body_ = &body;
+      n_ = n;
+      next_.store(0);
+      busy_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(mu_);
+    done_.wait(l, [this] { return busy_ == 0; });
+    body_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int64_t b = next_.fetch_add(16);
+      if (b >= n_) return;
+      const int64_t e = std::min(n_, b + 16);
+      for (int64_t i = b; i < e; ++i) (*body_)(i);
+    }
+  }
+  void worker() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(mu_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(mu_);
+      if (--busy_ == 0) done_.notify_one();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int64_t)>* body_ = nullptr;
+  int64_t n_ = 0;
+  std::atomic<int64_t> next_{0};
+  int busy_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // ------------------------------------------------------------------- chains
 struct Chain {
   rhmc_np::Legacy rng;
@@ -138,27 +208,17 @@ struct Run {
   int Kmax;
   BetaDist beta;
 
+  Pool* pool = nullptr;
+
   template <class F>
   void parallel(const std::vector<int64_t>& idx, F f) {
     const int64_t n = (int64_t)idx.size();
-    if (nt <= 1 || n < 32) {
+    if (!pool || pool->size() <= 1 || n < 32) {
       for (int64_t i = 0; i < n; ++i) f(idx[i]);
       return;
     }
-    std::atomic<int64_t> next{0};
-    auto work = [&]() {
-      for (;;) {
-        const int64_t b = next.fetch_add(16);
-        if (b >= n) return;
-        const int64_t e = std::min(n, b + 16);
-        for (int64_t i = b; i < e; ++i) f(idx[i]);
-      }
-    };
-    std::vector<std::thread> th;
-    const int m = (int)std::min<int64_t>(nt, (n + 15) / 16);
-    for (int t = 1; t < m; ++t) th.emplace_back(work);
-    work();
-    for (auto& t : th) t.join();
+    const std::function<void(int64_t)> body = [&](int64_t i) { f(idx[i]); };
+    pool->run(n, body);
   }
 
   // chains grouped by star count in order of first appearance
@@ -454,6 +514,8 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
   int nt = cfg->n_threads;
   if (nt <= 0) nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
   R.nt = nt;
+  Pool pool(nt);
+  R.pool = &pool;
   R.ch.resize((size_t)n);
   const int64_t W = 3 * (int64_t)cfg->N_max;
   std::vector<int64_t> all((size_t)n);
@@ -655,6 +717,37 @@ int engine_init(CtxEngine& E) {
   return 0;
 }
 
+// One 1-chain, 0-step trajectory of the run's first star count on each stream
+// the first time the process meets that (device, kernel): the first dispatch
+// of a kernel on a hardware queue set up its scratch and cost 6-8 ms inside a
+// run (profiles/r04_rj/trace).
+std::map<std::pair<int, int>, bool> g_warm;  // (device, K) under g_streams_mu
+
+int engine_warm(CtxEngine& E, const rhmc_params* P, int32_t K) {
+  int dev = 0;
+  RJ_HIP(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(g_streams_mu);
+  bool& done = g_warm[{dev, K}];
+  if (done) return 0;
+  double* d = nullptr;
+  std::vector<double> h(6 * (size_t)K, 0.0);  // q: stars of 1000 counts at (1 + k/2, 2), p = 0
+  for (int32_t k = 0; k < K; ++k) {
+    h[3 * k] = 1000.0;
+    h[3 * k + 1] = 1.0 + 0.5 * k;
+    h[3 * k + 2] = 2.0;
+  }
+  RJ_HIP(hipMalloc(&d, h.size() * sizeof(double)));
+  RJ_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+  int rc = 0;
+  for (int i = 0; i < kStreams && rc == 0; ++i)
+    rc = rhmc_leapfrog_device(E.ctx, P, d, d + 3 * K, 1, K, 0, nullptr, nullptr, E.s[i]);
+  for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(E.s[i]);
+  (void)hipFree(d);
+  if (rc) return rc;
+  done = true;
+  return 0;
+}
+
 int ctx_energy(void* user, const rhmc_params* P, const double* q, int64_t n, int32_t K,
                int32_t f_pos, double* V) {
   return rhmc_energy(static_cast<CtxEngine*>(user)->ctx, P, q, nullptr, V, nullptr, n, K, f_pos);
@@ -734,6 +827,8 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
     E.ctx = ctx;
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
     if (int rc = engine_init(E)) return rc;
+    if (n > 0)
+      if (int rc = engine_warm(E, P, K[0])) return rc;
     rhmc_rj_physics phys{&E, ctx_energy, ctx_steps};
     Run::Staged st;
     st.user = &E;
