@@ -2411,6 +2411,21 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   return RHMC_OK;
 }
 
+int rhmc_energy_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, const double* d_p,
+                       double* d_V, double* d_T, int64_t n_chains, int32_t K, int32_t f_pos,
+                       void* stream) {
+  int rc = check_common(ctx, n_chains, K);
+  if (rc) return rc;
+  if (n_chains == 0) return RHMC_OK;
+  if (!d_q) return fail(RHMC_ERR_ARG, "q is NULL");
+  if (d_T && !d_p) return fail(RHMC_ERR_ARG, "T requested but p is NULL");
+  Consts c;
+  if ((rc = make_consts(P, &c))) return rc;
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_energy(ctx, c, d_q, d_T ? d_p : nullptr, d_V, d_T, n_chains, K, f_pos, s);
+}
+
 int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q, const double* p, double* V,
                 double* T, int64_t n_chains, int32_t K, int32_t f_pos) {
   int rc = check_common(ctx, n_chains, K);

@@ -239,6 +239,7 @@ struct Run {
   }
 
   int energies(const std::vector<int64_t>& idx, std::vector<double>& V) {
+    if (staged.energy) return energies_staged(idx, V);
     std::vector<double> qb, vb;
     for (auto& grp : groups(idx)) {
       const int32_t K = grp.first;
@@ -264,8 +265,48 @@ struct Run {
     double* (*buffer)(void* user, size_t doubles) = nullptr;
     int (*launch)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
                   const int64_t* n, const size_t* off, int32_t n_steps) = nullptr;
+    // V of group g: q at off[g], V written at off[g] + n[g] 3 K[g]
+    int (*energy)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
+                  const int64_t* n, const size_t* off, int32_t f_pos) = nullptr;
   };
   Staged staged;
+
+  int energies_staged(const std::vector<int64_t>& idx, std::vector<double>& V) {
+    const auto gs = groups(idx);
+    if (gs.empty()) return 0;
+    const int32_t G = (int32_t)gs.size();
+    std::vector<int32_t> Ks((size_t)G);
+    std::vector<int64_t> ns((size_t)G);
+    std::vector<size_t> off((size_t)G);
+    size_t total = 0;
+    for (int32_t g = 0; g < G; ++g) {
+      Ks[g] = gs[g].first;
+      ns[g] = (int64_t)gs[g].second.size();
+      off[g] = total;
+      total += (size_t)ns[g] * (3 * (size_t)Ks[g] + 1);
+    }
+    double* h = staged.buffer(staged.user, total);
+    if (!h) return fail(RHMC_ERR_NOMEM, "staging buffer: " + g_err);
+    std::vector<int64_t> slots, slot_c;
+    std::vector<double*> slot_q, slot_v;
+    for (int32_t g = 0; g < G; ++g) {
+      const size_t d = 3 * (size_t)Ks[g];
+      for (size_t i = 0; i < gs[g].second.size(); ++i) {
+        slots.push_back((int64_t)slots.size());
+        slot_c.push_back(gs[g].second[i]);
+        slot_q.push_back(h + off[g] + i * d);
+        slot_v.push_back(h + off[g] + (size_t)ns[g] * d + i);
+      }
+    }
+    parallel(slots, [&](int64_t j) {
+      const Chain& c = ch[slot_c[j]];
+      std::memcpy(slot_q[j], c.q.data(), c.q.size() * 8);
+    });
+    const int rc = staged.energy(staged.user, &P, G, Ks.data(), ns.data(), off.data(), cfg->f_pos);
+    if (rc != 0) return engine_fail(rc, "energy");
+    for (size_t j = 0; j < slots.size(); ++j) V[slot_c[j]] = *slot_v[j];
+    return 0;
+  }
 
   int trajectories(const std::vector<int64_t>& idx) {
     if (staged.launch) return trajectories_staged(idx);
@@ -476,6 +517,7 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
           const uint32_t* seeds, int64_t n) {
   if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
   if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
+  if (cfg->n_pipes < 0 || cfg->n_pipes > 2) return fail(RHMC_ERR_ARG, "n_pipes must be 0, 1 or 2");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
   if (n > 0 && (!q || !K || !seeds)) return fail(RHMC_ERR_ARG, "q, K or seeds is NULL");
   if (cfg->n_iter < 0 || cfg->n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter or n_steps < 0");
@@ -499,10 +541,19 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
   return 0;
 }
 
+int host_threads(const rhmc_rj_config* cfg) {
+  const int nt = cfg->n_threads;
+  if (nt > 0) return nt;
+  return (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// n chains (a contiguous slice of the caller's: q, K, seeds point at its
+// first chain); record row l of chain c is l * rec_stride + rec_off + c; nt
+// host threads; the phase times are added to phase_out[7].
 int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_params* P0,
         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
-        const rhmc_rj_record* rec) {
-  if (int rc = check(P0, cfg, q, K, seeds, n)) return rc;
+        const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
+        double* phase_out) {
   if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
   Run R;
   R.phys = phys;
@@ -511,8 +562,6 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
   R.beta.set(cfg->beta_a, cfg->beta_b);
-  int nt = cfg->n_threads;
-  if (nt <= 0) nt = (int)std::min<unsigned>(16u, std::max(1u, std::thread::hardware_concurrency()));
   R.nt = nt;
   Pool pool(nt);
   R.pool = &pool;
@@ -564,7 +613,7 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
       h.E0 = V0[c] + T0[c];
-      const int64_t r = l * n + c;
+      const int64_t r = l * rec_stride + rec_off + c;
       if (rec) {
         if (rec->q_chain) {
           double* row = rec->q_chain + r * W;
@@ -620,7 +669,7 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
     // 7. accept / reject
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
-      const int64_t r = l * n + c;
+      const int64_t r = l * rec_stride + rec_off + c;
       bool acc = false;
       if (!h.dead) {
         const int64_t d = 3 * (int64_t)h.K;
@@ -647,8 +696,8 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
     });
     lap(6);
   }
-  if (rec && rec->phase_s)
-    for (int i = 0; i < 7; ++i) rec->phase_s[i] = phase[i];
+  if (phase_out)
+    for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];
   for (int64_t c = 0; c < n; ++c) {
     const Chain& h = R.ch[c];
     std::fill(q + c * W, q + (c + 1) * W, 0.);
@@ -679,6 +728,8 @@ std::map<int, DeviceStreams> g_streams;
 struct CtxEngine {
   rhmc_ctx* ctx = nullptr;
   hipStream_t s[kStreams] = {};
+  int ns = kStreams;             // streams in use: s[0 .. ns)
+  int dev = 0;
   double* d = nullptr;
   size_t d_bytes = 0;
   double* h = nullptr;
@@ -703,6 +754,7 @@ int engine_init(CtxEngine& E) {
   hipPointerAttribute_t at;
   RJ_HIP(hipPointerGetAttributes(&at, dimg));
   RJ_HIP(hipSetDevice(at.device));
+  E.dev = at.device;
   std::lock_guard<std::mutex> lock(g_streams_mu);
   DeviceStreams& ds = g_streams[at.device];
   if (!ds.warm) {
@@ -794,14 +846,31 @@ int ctx_launch(void* user, const rhmc_params* P, int32_t G, const int32_t* K, co
   for (int32_t i = 0; i < G && rc == 0; ++i) {  // largest groups first
     const int32_t g = order[i];
     const size_t sb = (size_t)n[g] * 3 * (size_t)K[g];
-    hipStream_t st = E.s[i % kStreams];
+    hipStream_t st = E.s[i % E.ns];
     double* hq = E.h + off[g];
     double* dq = E.d + off[g];
     RJ_HIP(hipMemcpyAsync(dq, hq, 2 * sb * 8, hipMemcpyHostToDevice, st));
     rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb, n[g], K[g], n_steps, nullptr, nullptr, st);
     if (rc == 0) RJ_HIP(hipMemcpyAsync(hq, dq, 2 * sb * 8, hipMemcpyDeviceToHost, st));
   }
-  for (auto& st : E.s) RJ_HIP(hipStreamSynchronize(st));
+  for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
+  return rc;
+}
+
+int ctx_energy_staged(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
+                      const int64_t* n, const size_t* off, int32_t f_pos) {
+  CtxEngine& E = *static_cast<CtxEngine*>(user);
+  int rc = 0;
+  for (int32_t g = 0; g < G && rc == 0; ++g) {
+    const size_t sb = (size_t)n[g] * 3 * (size_t)K[g];
+    hipStream_t st = E.s[g % E.ns];
+    double* hq = E.h + off[g];
+    double* dq = E.d + off[g];
+    RJ_HIP(hipMemcpyAsync(dq, hq, sb * 8, hipMemcpyHostToDevice, st));
+    rc = rhmc_energy_device(E.ctx, P, dq, nullptr, dq + sb, nullptr, n[g], K[g], f_pos, st);
+    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq + sb, dq + sb, (size_t)n[g] * 8, hipMemcpyDeviceToHost, st));
+  }
+  for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
   return rc;
 }
 
@@ -813,7 +882,32 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
                         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds,
                         int64_t n, const rhmc_rj_record* rec) {
   try {
-    return run(phys, nullptr, P, cfg, q, K, seeds, n, rec);
+    if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
+    double phase[7] = {0, 0, 0, 0, 0, 0, 0};
+    const int nt = host_threads(cfg);
+    int rc = 0;
+    if (cfg->n_pipes == 2 && n >= 2) {   // the callbacks are then called from two threads
+      const int64_t h = n / 2, W = 3 * (int64_t)cfg->N_max;
+      double phase1[7] = {0, 0, 0, 0, 0, 0, 0};
+      int rc1 = 0;
+      std::string err1;
+      std::thread t([&] {
+        rc1 = run(phys, nullptr, P, cfg, q + h * W, K + h, seeds + h, n - h, rec, n, h,
+                  std::max(1, nt / 2), phase1);
+        if (rc1) err1 = g_err;
+      });
+      rc = run(phys, nullptr, P, cfg, q, K, seeds, h, rec, n, 0, std::max(1, nt - nt / 2), phase);
+      t.join();
+      for (int i = 0; i < 7; ++i) phase[i] += phase1[i];
+      if (rc == 0 && rc1 != 0) {
+        g_err = err1;
+        rc = rc1;
+      }
+    } else {
+      rc = run(phys, nullptr, P, cfg, q, K, seeds, n, rec, n, 0, nt, phase);
+    }
+    if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
+    return rc;
   } catch (const std::exception& e) {
     return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
   }
@@ -823,18 +917,60 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
                 int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   try {
-    CtxEngine E;
-    E.ctx = ctx;
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
-    if (int rc = engine_init(E)) return rc;
+    CtxEngine E0, E1;
+    E0.ctx = E1.ctx = ctx;
+    if (int rc = engine_init(E0)) return rc;
     if (n > 0)
-      if (int rc = engine_warm(E, P, K[0])) return rc;
-    rhmc_rj_physics phys{&E, ctx_energy, ctx_steps};
-    Run::Staged st;
-    st.user = &E;
-    st.buffer = ctx_buffer;
-    st.launch = ctx_launch;
-    return run(&phys, &st, P, cfg, q, K, seeds, n, rec);
+      if (int rc = engine_warm(E0, P, K[0])) return rc;
+    int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 1024 ? 2 : 1);
+    if (pipes > 2 || n < 2) pipes = std::min(pipes, n < 2 ? 1 : 2);
+    const int nt = host_threads(cfg);
+    rhmc_rj_physics phys0{&E0, ctx_energy, ctx_steps}, phys1{&E1, ctx_energy, ctx_steps};
+    Run::Staged st0, st1;
+    st0.user = &E0;
+    st1.user = &E1;
+    for (Run::Staged* st : {&st0, &st1}) {
+      st->buffer = ctx_buffer;
+      st->launch = ctx_launch;
+      st->energy = ctx_energy_staged;
+    }
+    double phase[7] = {0, 0, 0, 0, 0, 0, 0};
+    int rc = 0;
+    if (pipes == 1) {
+      rc = run(&phys0, &st0, P, cfg, q, K, seeds, n, rec, n, 0, nt, phase);
+    } else {
+      // two halves, two host threads, two streams each (the HIP calls of the
+      // *_device entry points touch no shared context state)
+      const int64_t h = n / 2, W = 3 * (int64_t)cfg->N_max;
+      for (int i = 0; i < kStreams; ++i) E1.s[i] = E0.s[i];
+      E0.ns = E1.ns = kStreams / 2;
+      for (int i = 0; i < kStreams / 2; ++i) E1.s[i] = E0.s[kStreams / 2 + i];
+      const int nt1 = std::max(1, nt / 2), nt0 = std::max(1, nt - nt1);
+      double phase1[7] = {0, 0, 0, 0, 0, 0, 0};
+      int rc1 = 0;
+      std::string err1;
+      std::thread t([&] {
+        E1.dev = E0.dev;
+        if (hipSetDevice(E1.dev) != hipSuccess) {
+          rc1 = RHMC_ERR_HIP;
+          err1 = "hipSetDevice failed";
+          return;
+        }
+        rc1 = run(&phys1, &st1, P, cfg, q + h * W, K + h, seeds + h, n - h, rec, n, h, nt1,
+                  phase1);
+        if (rc1) err1 = g_err;
+      });
+      rc = run(&phys0, &st0, P, cfg, q, K, seeds, h, rec, n, 0, nt0, phase);
+      t.join();
+      for (int i = 0; i < 7; ++i) phase[i] += phase1[i];
+      if (rc == 0 && rc1 != 0) {
+        g_err = err1;
+        rc = rc1;
+      }
+    }
+    if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
+    return rc;
   } catch (const std::exception& e) {
     return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
   }

@@ -45,7 +45,8 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_ctx_create", "rhmc_ctx_set_image", "rhmc_ctx_image_device",
            "rhmc_ctx_destroy", "rhmc_ctx_synchronize", "rhmc_ctx_set_option",
            "rhmc_ctx_get_option", "rhmc_leapfrog",
-           "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_mh",
+           "rhmc_leapfrog_device", "rhmc_gradient", "rhmc_energy", "rhmc_energy_device",
+           "rhmc_mh",
            "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
            "rhmc_gen_image", "rhmc_gen_image_device", "rhmc_hmc_random",
            "rhmc_hmc_random_device", "rhmc_mh_scheduled", "rhmc_mh_scheduled_device")
@@ -139,6 +140,8 @@ def _load():
                                          ctypes.c_int32, ctypes.c_int32]),
         "rhmc_energy": (ctypes.c_int, [vp, P(RhmcParams), c_dp, c_dp, c_dp, c_dp,
                                        ctypes.c_int64, ctypes.c_int32, ctypes.c_int32]),
+        "rhmc_energy_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, vp, vp, ctypes.c_int64,
+                                              ctypes.c_int32, ctypes.c_int32, vp]),
         "rhmc_integrate": (ctypes.c_int, [vp, P(RhmcParams), ctypes.c_int32, c_dp, c_dp,
                                           ctypes.c_int64, ctypes.c_int32, ctypes.c_int32,
                                           ctypes.c_int32, c_ip]),
@@ -328,6 +331,14 @@ class Context:
                                          int(n_steps), ctypes.c_void_p(iters_ptr or 0),
                                          ctypes.c_void_p(status_ptr or 0),
                                          ctypes.c_void_p(stream or 0)))
+
+    def energy_device(self, params, q_ptr, p_ptr, V_ptr, T_ptr, n_chains, K, f_pos=0,
+                      stream=None):
+        """rhmc_energy_device: device pointers (p_ptr / T_ptr may be 0), f_pos bits."""
+        _check(_lib.rhmc_energy_device(self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr),
+                                       ctypes.c_void_p(p_ptr or 0), ctypes.c_void_p(V_ptr or 0),
+                                       ctypes.c_void_p(T_ptr or 0), int(n_chains), int(K),
+                                       int(f_pos), ctypes.c_void_p(stream or 0)))
 
     def gradient(self, params, q, kind=0):
         q2 = np.array(q, dtype=np.float64, order="C", copy=True)

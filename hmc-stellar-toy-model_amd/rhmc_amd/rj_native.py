@@ -36,7 +36,8 @@ class RjConfig(ctypes.Structure):
                 ("N_max", ctypes.c_int32), ("f_pos", ctypes.c_int32),
                 ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
                 ("n_threads", ctypes.c_int32), ("n_g_ff2", ctypes.c_int32),
-                ("n_beta", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("n_beta", ctypes.c_int32), ("n_pipes", ctypes.c_int32),
+                ("reserved", ctypes.c_int32),
                 ("P_move", ctypes.c_double * 3), ("fmin", ctypes.c_double),
                 ("fmax", ctypes.c_double), ("K_split", ctypes.c_double),
                 ("beta_a", ctypes.c_double), ("beta_b", ctypes.c_double),
@@ -99,7 +100,7 @@ def np_draws(seed, kind, n, a=0., b=0.):
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0):
+        n_threads=0, n_pipes=0):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
     vectors.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
@@ -132,7 +133,8 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     sb, nb = arr(schedule_beta)
     pm = (ctypes.c_double * 3)(*[float(v) for v in P_move])
     cfg = RjConfig(int(n_iter), int(n_steps), int(N_max), int(f_pos), int(rows), int(cols),
-                   int(n_threads), ng, nb, 0, pm, float(fmin), float(fmax), float(K_split),
+                   int(n_threads), ng, nb, int(n_pipes), 0, pm, float(fmin), float(fmax),
+                   float(K_split),
                    float(beta_a), float(beta_b), sg, sb)
     rows_n = int(n_iter) + 1
     rec = {"q_chain": np.zeros((rows_n, n, W)), "p_chain": np.zeros((rows_n, n, W)),

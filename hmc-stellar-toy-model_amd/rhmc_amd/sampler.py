@@ -672,7 +672,7 @@ class multi_gym(base_class):
     def run_RHMC_rj_batched(self, q_models_0, seeds, f_pos=True, delta=1e-6, Niter=100,
                             Nsteps=100, dt=1e-1, counter_max=1000, N_max=50,
                             P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None,
-                            engine="native", n_threads=0):
+                            engine="native", n_threads=0, n_pipes=0):
         """Many independent chains of run_RHMC WITH the reversible-jump moves
         (sampler_RHMC.py:937-1198; birth_death_move :1200-1270, split_merge_move
         :1273-1445), each chain at its own, changing, star count.  Chain c is
@@ -693,15 +693,18 @@ class multi_gym(base_class):
         (include/rhmc_rj.h): per-chain host work in C++ on n_threads host
         threads (0: up to 16) with a bit-identical replica of each chain's
         NumPy stream, and flag_chain [Niter+1, n] marks the iterations whose
-        proposal was a dead end (see the header); engine="python" is the NumPy
-        loop below (the reference's own draws through np.random)."""
+        proposal was a dead end (see the header); n_pipes = 2 (the default
+        from 1024 chains) runs the chains in two halves whose host and GPU
+        phases overlap, 1 keeps the engine batches of the NumPy loop;
+        engine="python" is the NumPy loop below (the reference's own draws
+        through np.random)."""
         n = len(q_models_0)
         if len(seeds) != n:
             raise ValueError("one seed per chain")
         if engine == "native":
             return self._rj_native(q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt,
                                    counter_max, N_max, P_move, schedule_g_ff2, schedule_beta,
-                                   n_threads)
+                                   n_threads, n_pipes)
         if engine != "python":
             raise ValueError("engine must be 'native' or 'python'")
         self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
@@ -812,7 +815,7 @@ class multi_gym(base_class):
         return q
 
     def _rj_native(self, q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt, counter_max, N_max,
-                   P_move, schedule_g_ff2, schedule_beta, n_threads):
+                   P_move, schedule_g_ff2, schedule_beta, n_threads, n_pipes=0):
         """run_RHMC_rj_batched through librhmc_rj.so (rhmc_rj_run)."""
         from . import rj_native
         self._check_geometry()
@@ -827,7 +830,8 @@ class multi_gym(base_class):
             P, q0, seeds, Niter, Nsteps, N_max, P_move, capi.V_FLUX_WALL if f_pos else 0,
             self.num_rows, self.num_cols, self.fmin if jumps else 1., self.fmax if jumps else 1.,
             self.K_split, self.beta_a, self.beta_b, schedule_g_ff2=schedule_g_ff2,
-            schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads)
+            schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads,
+            n_pipes=n_pipes)
         n_it = Niter + 1
         for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):
             if sched is not None and np.size(sched) > 0:    # the value of the last iteration

@@ -16,7 +16,7 @@
  *   rhmc_gradient
  *       base_class.dVdq (sampler_RHMC.py:365-425) and base_class.dphidq
  *       (:448-465), batched over chains.
- *   rhmc_energy
+ *   rhmc_energy / rhmc_energy_device
  *       base_class.V (sampler_RHMC.py:294-351) and base_class.T (:353-363)
  *       at H(q) (:229-258) — the trajectory-endpoint energies of the MH test
  *       (:1021-1026, :1070-1071).
@@ -229,6 +229,12 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
 int rhmc_energy(rhmc_ctx* ctx, const rhmc_params* P, const double* q,
                 const double* p, double* V, double* T, int64_t n_chains,
                 int32_t K, int32_t f_pos);
+/* Same on device-resident buffers (d_V or d_T may be NULL; d_p may be NULL
+ * when d_T is), asynchronous on `stream` (hipStream_t; NULL = the context's
+ * stream).  Launches on distinct streams may run concurrently. */
+int rhmc_energy_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
+                       const double* d_p, double* d_V, double* d_T, int64_t n_chains,
+                       int32_t K, int32_t f_pos, void* stream);
 
 /* n_steps steps of integrator `solver` (RHMC_SOLVER_*) on every chain; q, p
  * host [n_chains][3K], updated in place.  f_pos: the flux-wall momentum flip of

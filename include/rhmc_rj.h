@@ -15,8 +15,9 @@
  * their ln-acceptance factors) runs on a pool of host threads; every
  * trajectory and potential of an iteration phase is one engine call per
  * distinct star count (chains grouped by K in order of first appearance,
- * ascending chain index inside a group — the grouping of the Python
- * multi_gym.run_RHMC_rj_batched, so both see identical engine batches).
+ * ascending chain index inside a group — with n_pipes = 1 the grouping of the
+ * Python multi_gym.run_RHMC_rj_batched, so both see identical engine
+ * batches), the groups of a phase on concurrent HIP streams.
  *
  * Replaces: the per-chain Python loop of run_RHMC's reversible-jump branches
  * (one chain, one star count at a time) — this is its batched, native form.
@@ -70,6 +71,10 @@ typedef struct rhmc_rj_config {
   int32_t n_threads;     /* host worker threads; <= 0: min(hardware threads, 16)    */
   int32_t n_g_ff2;       /* schedule_g_ff2 length (0: none)                          */
   int32_t n_beta;        /* schedule_beta length (0: none)                           */
+  int32_t n_pipes;       /* 1: one pass over all chains per phase (the engine batches
+                            of multi_gym.run_RHMC_rj_batched); 2: the chains in two
+                            halves on two host threads, so one half's host work
+                            overlaps the other's GPU work; 0: 2 from 1024 chains    */
   int32_t reserved;      /* must be 0                                                */
   double P_move[3];      /* within / birth-death / split-merge probabilities         */
   double fmin, fmax;     /* power-law flux prior range, counts (:1221)               */
@@ -92,10 +97,10 @@ typedef struct rhmc_rj_record {
   int32_t* move;     /* 0 within, 1 birth, 2 death, 3 split, 4 merge      */
   int32_t* n_stars;  /* N_chain                                           */
   int32_t* flags;    /* RHMC_RJ_* bits of the iteration                   */
-  double* phase_s;   /* [7] wall seconds summed over the run: momentum +
-                        move draws (host), V(q), first trajectories,
-                        proposals (host), second trajectories, V(q'),
-                        accept (host)                                     */
+  double* phase_s;   /* [7] wall seconds summed over the run (and over the
+                        pipes): momentum + move draws (host), V(q), first
+                        trajectories, proposals (host), second
+                        trajectories, V(q'), accept (host)                */
 } rhmc_rj_record;
 
 #define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */

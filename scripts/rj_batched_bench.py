@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--nsteps", type=int, default=20)
     ap.add_argument("--engine", choices=("native", "python"), default="native")
     ap.add_argument("--threads", type=int, default=0, help="native host threads (0: up to 16)")
+    ap.add_argument("--pipes", type=int, default=0, help="native pipes (0: 2 from 1024 chains)")
     args = ap.parse_args()
     wl = workloads.make("B4", n_chains=args.chains)
     g = sampler.multi_gym(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
@@ -62,13 +63,13 @@ def main():
     t0 = time.perf_counter()
     g.run_RHMC_rj_batched(starts, list(range(args.chains)), Niter=args.niter,
                           Nsteps=args.nsteps, dt=0.05, N_max=120, P_move=[0.6, 0.2, 0.2],
-                          engine=args.engine, n_threads=args.threads)
+                          engine=args.engine, n_threads=args.threads, n_pipes=args.pipes)
     wall = time.perf_counter() - t0
     moves = g.move_chain
     steps = int(np.sum(np.where(moves == 0, 1, 2))) * args.nsteps
     out = {"what": "run_RHMC_rj_batched, big-sim4 geometry (32x32, K0 = 51), P_move "
                    "[0.6, 0.2, 0.2], one seeded stream per chain",
-           "engine": args.engine, "chains": args.chains, "iterations": args.niter + 1,
+           "engine": args.engine, "pipes": args.pipes, "chains": args.chains, "iterations": args.niter + 1,
            "nsteps": args.nsteps,
            "wall_s": wall, "ms_per_iteration": wall / (args.niter + 1) * 1e3,
            "chain_leapfrog_steps_per_s": steps / wall,

@@ -106,3 +106,32 @@ def test_native_dead_ends_on_the_engine(gpu_lib):
     assert not g.A_chain[g.flag_chain.astype(bool)].any()
     assert (g.N_chain >= 1).all() and (g.N_chain <= 4).all()
     assert all(np.isfinite(x).all() and 3 <= x.size <= 12 for x in q)
+
+
+def test_native_two_pipes_equal_one(gpu_lib):
+    """n_pipes = 2 (two halves on two host threads, their host and GPU phases
+    overlapping, each half its own engine batches) gives every chain the same
+    moves, star counts and accepts as one pass, and the same states (the
+    engine's results do not depend on the batch; tolerance for the kernels
+    whose last bits follow wave-mates in rare non-finite / far-off cases)."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+
+    def make():
+        g = _gym(par)
+        g.D = z[name + "/D"]
+        return g
+    rs = np.random.RandomState(9)
+    starts = _starts(z[name + "/q_model"], 64, rs)
+    kw = dict(f_pos=True, delta=1e-6, Niter=8, Nsteps=6, dt=0.05, N_max=16,
+              P_move=[0.4, 0.3, 0.3])
+    a, b = make(), make()
+    qa = a.run_RHMC_rj_batched([m.copy() for m in starts], list(range(64)), n_pipes=1, **kw)
+    qb = b.run_RHMC_rj_batched([m.copy() for m in starts], list(range(64)), n_pipes=2, **kw)
+    for k in ("move_chain", "N_chain", "A_chain", "flag_chain"):
+        np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+    assert_state_close(a.q_chain, b.q_chain, 1e-12, "q_chain")
+    np.testing.assert_allclose(a.E_chain, b.E_chain, rtol=1e-12)
+    for x, y in zip(qa, qb):
+        np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)

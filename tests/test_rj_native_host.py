@@ -79,7 +79,7 @@ def test_scipy_beta_rvs_is_the_replica(rj):
     assert a == r.beta(2., 2.)
 
 
-def _native(rj, g, starts, seeds, kw, n_threads=4):
+def _native(rj, g, starts, seeds, kw, n_threads=4, n_pipes=1):
     from rhmc_amd import capi
     qms = [g.format_q(m.copy()) for m in starts]
     P = g._params(for_energy=True)
@@ -92,7 +92,7 @@ def _native(rj, g, starts, seeds, kw, n_threads=4):
     return rj.run(P, qms, seeds, kw["Niter"], kw["Nsteps"], kw["N_max"], kw["P_move"],
                   capi.V_FLUX_WALL if kw["f_pos"] else 0, g.num_rows, g.num_cols, g.fmin, g.fmax,
                   g.K_split, g.beta_a, g.beta_b, physics=(lambda q, fp: fake_V(q), steps),
-                  n_threads=n_threads)
+                  n_threads=n_threads, n_pipes=n_pipes)
 
 
 def _clean(g, N_max):
@@ -140,15 +140,19 @@ def test_native_equals_python_batched(rj, P_move):
 def test_dead_ends_are_rejected_and_threads_do_not_matter(rj):
     """Deaths / merges at one star: the native driver rejects them (flag
     DEAD_END, state back to the iteration's start, no accept draw) and every
-    chain's record is independent of the host thread count."""
+    chain's record is independent of the host thread count and of the split
+    into two pipes (with these stand-ins every chain's physics is its own)."""
     starts = [np.array([[18.5, 16., 16.]])] * 20 + STARTS * 5
     seeds = list(range(100, 100 + len(starts)))
     kw = dict(f_pos=True, Niter=25, Nsteps=2, dt=0.05, N_max=6, P_move=[0.2, 0.4, 0.4])
     _, r1 = _native(rj, _gym(), starts, seeds, kw, n_threads=1)
     q4, r4 = _native(rj, _gym(), starts, seeds, kw, n_threads=7)
+    q2, r2 = _native(rj, _gym(), starts, seeds, kw, n_threads=5, n_pipes=2)   # two halves
     for k in r1:
         if k != "phase_s":                            # wall times
             assert np.array_equal(r1[k], r4[k]), k
+            assert np.array_equal(r1[k], r2[k]), k
+    assert all(np.array_equal(a, b) for a, b in zip(q4, q2))
     assert (r1["phase_s"] >= 0).all() and r1["phase_s"].sum() > 0
     fl = r1["flags"].astype(bool)
     assert fl.any()
