@@ -826,12 +826,15 @@ class multi_gym(base_class):
             assert False                                  # :1205-1207 (prior required)
         q0 = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
         P = self._params(delta, counter_max, for_energy=True)
+        import time
+        t0 = time.perf_counter()
         q_end, rec = rj_native.run(
             P, q0, seeds, Niter, Nsteps, N_max, P_move, capi.V_FLUX_WALL if f_pos else 0,
             self.num_rows, self.num_cols, self.fmin if jumps else 1., self.fmax if jumps else 1.,
             self.K_split, self.beta_a, self.beta_b, schedule_g_ff2=schedule_g_ff2,
             schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads,
             n_pipes=n_pipes)
+        self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
         for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):
             if sched is not None and np.size(sched) > 0:    # the value of the last iteration

@@ -73,6 +73,9 @@ def main():
            "nsteps": args.nsteps,
            "wall_s": wall, "ms_per_iteration": wall / (args.niter + 1) * 1e3,
            "chain_leapfrog_steps_per_s": steps / wall,
+           "native_call_s": getattr(g, "rj_native_s", None) if args.engine == "native" else None,
+           "chain_leapfrog_steps_per_s_native_call": (steps / g.rj_native_s
+                                                      if args.engine == "native" else None),
            "gpu_call_share": gpu["s"] / wall if args.engine == "python" else None,
            "gpu_calls": gpu["calls"] if args.engine == "python" else None,
            "accepted_jumps": int(np.sum(g.A_chain & (moves > 0))),
