@@ -55,8 +55,10 @@
  *     (passed as void*, NULL = the context's stream) and are asynchronous.
  *   - Every call returns 0 on success or a negative RHMC_ERR_* code;
  *     rhmc_last_error() gives a thread-local message.  No C++ exception
- *     crosses the ABI.  A context must not be used by two threads at once;
- *     one context per GPU.
+ *     crosses the ABI.  A context must not be used by two threads at once,
+ *     except that rhmc_leapfrog_device and rhmc_energy_device (which keep no
+ *     per-call state in the context) may be called from several threads on
+ *     distinct streams; one context per GPU.
  */
 #ifndef RHMC_H
 #define RHMC_H

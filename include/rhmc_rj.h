@@ -17,7 +17,9 @@
  * distinct star count (chains grouped by K in order of first appearance,
  * ascending chain index inside a group — with n_pipes = 1 the grouping of the
  * Python multi_gym.run_RHMC_rj_batched, so both see identical engine
- * batches), the groups of a phase on concurrent HIP streams.
+ * batches), the groups of a phase on concurrent HIP streams (through
+ * rhmc_leapfrog_device / rhmc_energy_device, the entry points rhmc.h allows
+ * from several threads at once).
  *
  * Replaces: the per-chain Python loop of run_RHMC's reversible-jump branches
  * (one chain, one star count at a time) — this is its batched, native form.
