@@ -1,0 +1,190 @@
+// Host AddressSanitizer driver for librhmc_rj (include/rhmc_rj.h), no GPU:
+// rhmc_rj_run_physics with deterministic C stand-ins for the two engine calls
+// (the same ones as tests/test_rj_batched_host.py's), over every move mix,
+// one and two pipes, dead ends, schedules, records on and off, every error
+// path, and the NumPy-stream replica.  Built by `make -C
+// hmc-stellar-toy-model_amd/host asan` and run by tests/test_rj_asan_host.py;
+// prints "rj asan ok" when every check passed.
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "rhmc_rj.h"
+
+static int g_fail = 0;
+#define CHECK(cond, what)                                               \
+  do {                                                                  \
+    if (!(cond)) {                                                      \
+      std::printf("FAIL %s (%s) %s\n", what, #cond, rhmc_rj_last_error()); \
+      ++g_fail;                                                         \
+    }                                                                   \
+  } while (0)
+
+// V = 1e-4 sum q^2; steps: q += 0.01 p, p = 0.99 p - 1e-4 q
+static int fake_energy(void*, const rhmc_params*, const double* q, int64_t n, int32_t K, int32_t,
+                       double* V) {
+  for (int64_t c = 0; c < n; ++c) {
+    double s = 0;
+    for (int32_t i = 0; i < 3 * K; ++i) s += q[c * 3 * K + i] * q[c * 3 * K + i];
+    V[c] = 1e-4 * s;
+  }
+  return 0;
+}
+static int fake_steps(void*, const rhmc_params*, double* q, double* p, int64_t n, int32_t K,
+                      int32_t n_steps) {
+  for (int s = 0; s < n_steps; ++s)
+    for (int64_t e = 0; e < n * 3 * K; ++e) {
+      q[e] = q[e] + 0.01 * p[e];
+      p[e] = 0.99 * p[e] - 1e-4 * q[e];
+    }
+  return 0;
+}
+static int bad_steps(void*, const rhmc_params*, double*, double*, int64_t, int32_t, int32_t) {
+  return RHMC_ERR_HIP;
+}
+
+static rhmc_params params() {
+  rhmc_params P;
+  std::memset(&P, 0, sizeof(P));
+  P.dt = 0.05;
+  P.delta = 1e-6;
+  P.B_count = 24.98145266935892;
+  P.f_lim = P.B_count;
+  P.f_low = 3.9592934273456466;
+  P.fwhm_pix = 3.4999999999999996;
+  P.g_xx = 0.05;
+  P.g_ff = 4.;
+  P.g_ff2 = 4.;
+  P.g0 = 0.035997054345069765;
+  P.g1 = 0.4523523265306124;
+  P.g2 = 0.008141675878296745;
+  P.alpha = 2.;
+  P.beta = 1.;
+  P.Vc_r_pow = 1.;
+  P.V_prior_const = 1.5;
+  P.counter_max = 1000;
+  P.use_prior = 1;
+  return P;
+}
+
+static rhmc_rj_config config(int n_iter, int N_max, double p0, double p1, double p2) {
+  rhmc_rj_config c;
+  std::memset(&c, 0, sizeof(c));
+  c.n_iter = n_iter;
+  c.n_steps = 3;
+  c.N_max = N_max;
+  c.f_pos = 1;
+  c.rows = c.cols = 32;
+  c.n_threads = 3;
+  c.P_move[0] = p0;
+  c.P_move[1] = p1;
+  c.P_move[2] = p2;
+  c.fmin = 395.92934273456467;
+  c.fmax = 39592.93427345646;
+  c.K_split = 1.;
+  c.beta_a = c.beta_b = 2.;
+  return c;
+}
+
+struct Rec {
+  std::vector<double> q, p, E, V, T, ph;
+  std::vector<int32_t> a, m, ns, fl;
+  rhmc_rj_record r;
+  Rec(int rows, int n, int W)
+      : q((size_t)rows * n * W), p((size_t)rows * n * W), E((size_t)rows * n), V(E.size()),
+        T(E.size()), ph(7), a(E.size()), m(E.size()), ns(E.size()), fl(E.size()) {
+    r = {q.data(), p.data(), E.data(), V.data(), T.data(), a.data(), m.data(), ns.data(),
+         fl.data(), ph.data()};
+  }
+};
+
+int main() {
+  const rhmc_params P = params();
+  rhmc_rj_physics phys{nullptr, fake_energy, fake_steps};
+  const int n = 37;
+  for (int mix = 0; mix < 3; ++mix)
+    for (int pipes = 1; pipes <= 2; ++pipes)
+      for (int with_rec = 0; with_rec < 2; ++with_rec) {
+        rhmc_rj_config c = mix == 0 ? config(15, 6, 0.4, 0.3, 0.3)
+                           : mix == 1 ? config(15, 6, 0.2, 0.8, 0.0)
+                                      : config(15, 6, 0.2, 0.0, 0.8);
+        c.n_pipes = pipes;
+        const double sched[3] = {1., 2., 4.};
+        if (mix == 0) {
+          c.schedule_g_ff2 = sched;
+          c.n_g_ff2 = 3;
+          c.schedule_beta = sched;
+          c.n_beta = 2;
+        }
+        const int W = 3 * c.N_max;
+        std::vector<double> q((size_t)n * W, 0.);
+        std::vector<int32_t> K(n);
+        std::vector<uint32_t> seeds(n);
+        for (int i = 0; i < n; ++i) {
+          K[i] = 1 + i % 4;                 // one-star chains meet dead ends
+          seeds[i] = 100u + (uint32_t)i;
+          for (int k = 0; k < K[i]; ++k) {
+            q[(size_t)i * W + 3 * k] = 500. + 300. * k;
+            q[(size_t)i * W + 3 * k + 1] = 5. + 4. * k;
+            q[(size_t)i * W + 3 * k + 2] = 20. - 3. * k;
+          }
+        }
+        Rec R(c.n_iter + 1, n, W);
+        const int rc = rhmc_rj_run_physics(&phys, &P, &c, q.data(), K.data(), seeds.data(), n,
+                                           with_rec ? &R.r : nullptr);
+        CHECK(rc == 0, "run");
+        for (int i = 0; i < n; ++i) CHECK(K[i] >= 1 && K[i] <= c.N_max, "star count range");
+      }
+  // errors
+  {
+    rhmc_rj_config c = config(2, 4, 0.5, 0.25, 0.25);
+    std::vector<double> q(12, 1.);
+    int32_t K = 2;
+    uint32_t s = 1;
+    CHECK(rhmc_rj_run_physics(&phys, nullptr, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "null params");
+    CHECK(rhmc_rj_run_physics(nullptr, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "null physics");
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, nullptr, &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "null q");
+    c.P_move[0] = 0.9;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "P_move sum");
+    c = config(2, 4, 0.5, 0.25, 0.25);
+    c.reserved = 1;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "reserved");
+    c = config(2, 4, 0.5, 0.25, 0.25);
+    c.n_pipes = 3;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "n_pipes");
+    c = config(2, 4, 0.5, 0.25, 0.25);
+    K = 5;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "K > N_max");
+    K = 2;
+    c.n_g_ff2 = 2;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
+          "schedule NULL");
+    c = config(2, 4, 0.5, 0.25, 0.25);
+    rhmc_rj_physics bad{nullptr, fake_energy, bad_steps};
+    CHECK(rhmc_rj_run_physics(&bad, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_HIP,
+          "engine failure");
+    CHECK(rhmc_rj_run(nullptr, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG, "null ctx");
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 0, nullptr) == 0, "n = 0");
+  }
+  // the stream replica
+  std::vector<double> d(1000);
+  for (int kind = 0; kind <= 5; ++kind)
+    CHECK(rhmc_np_draws(7, kind, kind == 2 ? 51. : 2., 2., 1000, d.data()) == 0, "draws");
+  CHECK(rhmc_np_draws(7, 9, 0., 0., 10, d.data()) == RHMC_ERR_ARG, "bad kind");
+  CHECK(rhmc_np_draws(7, 0, 0., 0., 10, nullptr) == RHMC_ERR_ARG, "null out");
+  if (g_fail) {
+    std::printf("%d failures\n", g_fail);
+    return 1;
+  }
+  std::printf("rj asan ok\n");
+  return 0;
+}
