@@ -100,8 +100,45 @@ struct Rec {
   }
 };
 
-int main() {
+// gpu mode: rhmc_rj_run on a real context (the staged, stream-concurrent
+// engine path, one and two pipes) on a synthetic 32x32 image
+static void gpu_mode(const rhmc_params& P) {
+  std::vector<double> D(32 * 32);
+  for (int i = 0; i < 32 * 32; ++i) D[i] = 25. + (i % 7);
+  rhmc_ctx* ctx = nullptr;
+  CHECK(rhmc_ctx_create(0, D.data(), 32, 32, &ctx) == 0, "ctx create");
+  if (!ctx) return;
+  const int n = 45;
+  for (int pipes = 1; pipes <= 2; ++pipes) {
+    rhmc_rj_config c = config(6, 16, 0.4, 0.3, 0.3);
+    c.n_pipes = pipes;
+    const int W = 3 * c.N_max;
+    std::vector<double> q((size_t)n * W, 0.);
+    std::vector<int32_t> K(n);
+    std::vector<uint32_t> seeds(n);
+    for (int i = 0; i < n; ++i) {
+      K[i] = 1 + i % 13;                 // one-star, pixel-major and dense kernels
+      seeds[i] = 300u + (uint32_t)i;
+      for (int k = 0; k < K[i]; ++k) {
+        q[(size_t)i * W + 3 * k] = 800. + 200. * k;
+        q[(size_t)i * W + 3 * k + 1] = 4. + 2. * k;
+        q[(size_t)i * W + 3 * k + 2] = 27. - 2. * k;
+      }
+    }
+    Rec R(c.n_iter + 1, n, W);
+    CHECK(rhmc_rj_run(ctx, &P, &c, q.data(), K.data(), seeds.data(), n, &R.r) == 0, "gpu run");
+    for (int i = 0; i < n; ++i) CHECK(K[i] >= 1 && K[i] <= c.N_max, "gpu star count range");
+  }
+  rhmc_ctx_destroy(ctx);
+}
+
+int main(int argc, char** argv) {
   const rhmc_params P = params();
+  if (argc > 1 && std::strcmp(argv[1], "gpu") == 0) {
+    gpu_mode(P);
+    std::printf(g_fail ? "%d failures\n" : "rj asan gpu ok\n", g_fail);
+    return g_fail ? 1 : 0;
+  }
   rhmc_rj_physics phys{nullptr, fake_energy, fake_steps};
   const int n = 37;
   for (int mix = 0; mix < 3; ++mix)

@@ -25,3 +25,17 @@ def test_rj_driver_under_asan():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "rj asan ok" in r.stdout
     assert "AddressSanitizer" not in r.stderr
+
+
+@pytest.mark.gpu
+def test_rj_driver_on_the_engine_under_asan(gpu_lib):
+    """rhmc_rj_run on a real context (staged groups on concurrent streams,
+    one and two pipes, K from 1 to 13) with the driver's host code under ASan;
+    leak detection off (the HIP runtime keeps process-lifetime allocations)."""
+    if not os.path.exists(BIN):
+        pytest.skip("build/asan/rj_asan not built (make -C hmc-stellar-toy-model_amd/host asan)")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1")
+    r = subprocess.run([BIN, "gpu"], capture_output=True, text=True, env=env, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "rj asan gpu ok" in r.stdout
+    assert "AddressSanitizer" not in r.stderr
