@@ -135,3 +135,44 @@ def test_native_two_pipes_equal_one(gpu_lib):
     np.testing.assert_allclose(a.E_chain, b.E_chain, rtol=1e-12)
     for x, y in zip(qa, qb):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("golden,name", [("rj", "rj_bd"), ("rj", "rj_sm"), ("rj", "rj_all"),
+                                         ("mh", "mh1"), ("mh", "mh3"), ("mh_sched", "g1"),
+                                         ("mh_sched", "g3"), ("mh_sched", "g3vc")])
+def test_native_reproduces_reference_goldens(gpu_lib, golden, name):
+    """Every reference run_RHMC golden (birth/death only, split/merge only,
+    all moves; within-model MH with one and three stars; g_ff2 / beta
+    schedules with and without repulsion) through the native driver as chain
+    0 of a batch of six (the other five: the same start on other seeds, which
+    share its engine batches): moves, star counts and accepts exact, states
+    and energies to the reference tolerances."""
+    from test_gpu_sampler import _sched_gym
+    z = load_golden(golden)
+    kw = dict(f_pos=True, delta=1e-6, Niter=int(z[name + "/niter"]),
+              Nsteps=int(z[name + "/nsteps"]), dt=float(z[name + "/dt"]))
+    if golden == "mh_sched":
+        g, sg, sb = _sched_gym(z, name)
+        kw.update(schedule_g_ff2=sg, schedule_beta=sb)
+    else:
+        g = _gym(R.params_from_npz(z, name + "/par_"))
+        g.D = z[name + "/D"]
+    qm = z[name + "/q_model"]
+    if golden == "rj":
+        kw.update(N_max=int(z[name + "/N_max"]), P_move=list(z[name + "/P_move"]))
+    else:
+        kw.update(N_max=qm.shape[0], P_move=[1., 0., 0.])
+    seed = int(z[name + "/seed"])
+    g.run_RHMC_rj_batched([qm.copy() for _ in range(6)], [seed] + [seed + 1 + i for i in range(5)],
+                          n_pipes=1, **kw)
+    np.testing.assert_array_equal(g.A_chain[:, 0].astype(np.int32), z[name + "/A_chain"])
+    if golden == "rj":
+        np.testing.assert_array_equal(g.move_chain[:, 0], z[name + "/move_chain"])
+        np.testing.assert_array_equal(g.N_chain[:, 0], z[name + "/N_chain"])
+    W = z[name + "/q_chain"].shape[-1]
+    assert_state_close(g.q_chain[:, 0, :W], z[name + "/q_chain"], 1e-9, "q_chain")
+    assert_state_close(g.p_chain[:, 0, :W], z[name + "/p_chain"], 1e-9, "p_chain")
+    np.testing.assert_allclose(g.E_chain[:, 0], z[name + "/E_chain"], rtol=1e-11)
+    np.testing.assert_allclose(g.V_chain[:, 0], z[name + "/V_chain"], rtol=1e-11)
+    if golden == "mh_sched":
+        assert g.g_ff2 == z[name + "/g_ff2_final"] and g.beta == z[name + "/beta_final"]
