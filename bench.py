@@ -300,6 +300,78 @@ def bench_datagen(args, wl, P, ctx, dev, stream, world, rank):
         dist.destroy_process_group()
 
 
+def bench_rj(args, wl, gpu, world, rank):
+    """--mode rj: the reversible-jump sampler (multi_gym.run_RHMC with P_move
+    = [0.6, 0.2, 0.2], sampler_RHMC.py:937-1198) through the native driver
+    librhmc_rj.so on this rank's chains, each on its own seeded NumPy-stream
+    replica; one bench step = one run of --mh-iter iterations of --leap steps
+    per trajectory.  A move-0 iteration counts --leap chain-leapfrog-steps, a
+    jump 2 x --leap (its two trajectories).  Host work and GPU phases
+    interleave, so there is no single dominant kernel: roofline null."""
+    import numpy as np
+    import torch.distributed as dist
+    from rhmc_amd import sampler, shard
+    from rhmc_amd.photometry import mag2flux
+    g = sampler.multi_gym(dt=0.05, g_xx=float(wl.params["g_xx"]), g_ff=float(wl.params["g_ff"]),
+                          g_ff2=float(wl.params["g_ff2"]))
+    g.num_rows, g.num_cols = wl.D.shape
+    g.use_prior, g.alpha = True, 2.
+    g.fmin = mag2flux(23.3) * g.flux_to_count
+    g.fmax = mag2flux(15.) * g.flux_to_count
+    g.D = wl.D
+    g.device = gpu
+    starts = []
+    for c in range(wl.n_chains):
+        m = wl.q0[c].reshape(-1, 3).copy()
+        m[:, 0] = np.minimum(g.flux2mag_converter(m[:, 0]), 22.5)   # above the flux wall
+        starts.append(m)
+    leap = args.leap or 20
+    n_it = args.mh_iter
+    kw = dict(Niter=n_it - 1, Nsteps=leap, dt=0.05, N_max=min(256, 2 * wl.K + 20),
+              P_move=[0.6, 0.2, 0.2])
+    seeds = [1000 * rank + c for c in range(wl.n_chains)]
+    for _ in range(args.warmup):
+        g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, **kw)
+    if world > 1:
+        dist.barrier()
+    steps = 0
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        g.run_RHMC_rj_batched([m.copy() for m in starts], [s + 7 * (i + 1) for s in seeds], **kw)
+        steps += int(np.sum(np.where(g.move_chain == 0, 1, 2))) * leap
+    wall = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        wall = shard.max_over_ranks(wall)
+        steps = int(shard.sum_over_ranks(steps))
+    res = {
+        "metric": "chain-leapfrog-steps/sec, reversible-jump run_RHMC (%s %dx%d, K0=%d, "
+                  "%d chains/GPU)" % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K, wl.n_chains),
+        "value": steps / wall, "unit": "chain-leapfrog-steps/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (%s image and starts, chain seeds 1000 rank + c)" % wl.name,
+        "config": {"workload": "%s: %dx%d image, K0=%d, %d chains/GPU, %d iterations of %d "
+                               "steps per run, P_move [0.6, 0.2, 0.2], N_max %d"
+                               % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K, wl.n_chains,
+                                  n_it, leap, kw["N_max"]), "mode": "rj",
+                   "parallelism": "chain-sharded x%d" % world},
+        "roofline": None,
+        "rj": {"accept_rate_jumps": float(np.mean(g.A_chain[g.move_chain > 0]))
+               if (g.move_chain > 0).any() else None,
+               "star_counts_end": [int(g.N_chain[-1].min()), int(g.N_chain[-1].max())],
+               "dead_end_iterations": int(np.sum(g.flag_chain != 0)),
+               "phase_ms_per_iteration": {k: v * 1e3 / n_it for k, v in g.rj_phase_s.items()},
+               "native_call_s_last": g.rj_native_s},
+        "cpu_baseline": None,
+        "sources": source_hash(),
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None,
@@ -314,7 +386,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true",
                     help="skip the host-buffer (rhmc_leapfrog, PCIe-inclusive) measurement")
-    ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "hmc_random", "datagen"),
+    ap.add_argument("--mode", choices=("leapfrog", "mh", "integrate", "hmc_random", "datagen",
+                                       "rj"),
                     default="leapfrog",
                     help="mh: whole MH iterations on device (momentum draw, V+T, accept; "
                          "Philox RNG); one bench step = --mh-iter iterations of --leap steps. "
@@ -322,7 +395,9 @@ def main():
                          "hmc_random: samplers.HMC_random trajectories of --leap steps "
                          "(rhmc_hmc_random). "
                          "datagen: --n-real Poisson realisations of the workload's model "
-                         "image (rhmc_gen_image)")
+                         "image (rhmc_gen_image). "
+                         "rj: the reversible-jump run_RHMC through librhmc_rj.so, one step "
+                         "= --mh-iter iterations of --leap steps (default workload: use B4)")
     ap.add_argument("--mh-iter", type=int, default=10)
     ap.add_argument("--f-pos", type=int, choices=(0, 1), default=1,
                     help="--mode mh: run_RHMC's f_pos (V = inf below the flux wall, "
@@ -386,6 +461,9 @@ def main():
 
     if world > 1:
         init_gloo(args.timeout)
+    if args.mode == "rj":
+        return bench_rj(args, wl, int(os.environ.get("RHMC_BENCH_DEVICE", local_rank)), world,
+                        rank)
     ndev = torch.cuda.device_count()
     if gpu >= ndev:
         raise SystemExit("bench.py: rank %d wants GPU %d but %d are visible"

@@ -46,3 +46,13 @@ def max_over_ranks(value, dist=None):
     t = torch.tensor([float(value)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def sum_over_ranks(value, dist=None):
+    """Sum of a host number over all ranks (e.g. the chain-steps each rank did)."""
+    import torch
+    if dist is None:
+        import torch.distributed as dist
+    t = torch.tensor([float(value)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
