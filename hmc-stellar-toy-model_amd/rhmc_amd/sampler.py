@@ -216,6 +216,16 @@ class base_class(object):
             q[i, 0] = self.mag2flux_converter(q[i, 0])
         return q.reshape((q.size,))
 
+    def _format_q_fast(self, q_model):
+        """format_q on a copy, per star with Python floats: the same pow and
+        product per element as mag2flux_converter (bit-equal), ~4x faster than
+        the np.float64 scalar loop (the batched drivers convert thousands of
+        chains)."""
+        q = np.array(q_model, dtype=np.float64)
+        ftc = self.flux_to_count
+        q[:, 0] = [10 ** (0.4 * (22.5 - v)) * ftc for v in q[:, 0].tolist()]
+        return q.reshape(-1)
+
     def reverse_format_q(self, q):
         """sampler_RHMC.py:219-227"""
         q = np.copy(q.reshape((-1, 3)))
@@ -824,7 +834,7 @@ class multi_gym(base_class):
         jumps = P_move[1] != 0 or P_move[2] != 0
         if jumps and (self.alpha is None or self.fmin is None or self.fmax is None):
             assert False                                  # :1205-1207 (prior required)
-        q0 = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
+        q0 = [self._format_q_fast(m) for m in q_models_0]
         P = self._params(delta, counter_max, for_energy=True)
         import time
         t0 = time.perf_counter()

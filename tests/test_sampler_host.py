@@ -137,3 +137,14 @@ def test_vectorised_H_is_bit_identical():
         q[1::3] = rs.uniform(0, 32, K)
         q[2::3] = rs.uniform(0, 32, K)
         assert np.array_equal(g._H_vec(q), g.H(q, grad=False))
+
+
+def test_format_q_fast_is_bit_identical():
+    """The batched native RJ driver converts magnitudes with _format_q_fast:
+    bit for bit format_q (sampler_RHMC.py:209-217)."""
+    from rhmc_amd import sampler
+    g = sampler.multi_gym()
+    rs = np.random.RandomState(5)
+    for K in (1, 3, 51, 120):
+        m = np.column_stack([rs.uniform(14, 24, K), rs.uniform(0, 48, K), rs.uniform(0, 48, K)])
+        assert np.array_equal(g._format_q_fast(m), g.format_q(m.copy()))
