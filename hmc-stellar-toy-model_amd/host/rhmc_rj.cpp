@@ -734,7 +734,9 @@ struct CtxEngine {
   size_t d_bytes = 0;
   double* h = nullptr;
   size_t h_bytes = 0;
-  ~CtxEngine() {
+  ~CtxEngine() {  // nothing may still be copying into the buffers (error paths)
+    for (int i = 0; i < ns; ++i)
+      if (s[i]) (void)hipStreamSynchronize(s[i]);
     if (d) (void)hipFree(d);
     if (h) (void)hipHostFree(h);
   }
@@ -849,9 +851,12 @@ int ctx_launch(void* user, const rhmc_params* P, int32_t G, const int32_t* K, co
     hipStream_t st = E.s[i % E.ns];
     double* hq = E.h + off[g];
     double* dq = E.d + off[g];
-    RJ_HIP(hipMemcpyAsync(dq, hq, 2 * sb * 8, hipMemcpyHostToDevice, st));
-    rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb, n[g], K[g], n_steps, nullptr, nullptr, st);
-    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq, dq, 2 * sb * 8, hipMemcpyDeviceToHost, st));
+    hipError_t e = hipMemcpyAsync(dq, hq, 2 * sb * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb, n[g], K[g], n_steps, nullptr, nullptr, st);
+      if (rc == 0) e = hipMemcpyAsync(hq, dq, 2 * sb * 8, hipMemcpyDeviceToHost, st);
+    }
+    if (e != hipSuccess) rc = fail(RHMC_ERR_HIP, std::string("staging copy: ") + hipGetErrorString(e));
   }
   for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
   return rc;
@@ -866,9 +871,12 @@ int ctx_energy_staged(void* user, const rhmc_params* P, int32_t G, const int32_t
     hipStream_t st = E.s[g % E.ns];
     double* hq = E.h + off[g];
     double* dq = E.d + off[g];
-    RJ_HIP(hipMemcpyAsync(dq, hq, sb * 8, hipMemcpyHostToDevice, st));
-    rc = rhmc_energy_device(E.ctx, P, dq, nullptr, dq + sb, nullptr, n[g], K[g], f_pos, st);
-    if (rc == 0) RJ_HIP(hipMemcpyAsync(hq + sb, dq + sb, (size_t)n[g] * 8, hipMemcpyDeviceToHost, st));
+    hipError_t e = hipMemcpyAsync(dq, hq, sb * 8, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+      rc = rhmc_energy_device(E.ctx, P, dq, nullptr, dq + sb, nullptr, n[g], K[g], f_pos, st);
+      if (rc == 0) e = hipMemcpyAsync(hq + sb, dq + sb, (size_t)n[g] * 8, hipMemcpyDeviceToHost, st);
+    }
+    if (e != hipSuccess) rc = fail(RHMC_ERR_HIP, std::string("staging copy: ") + hipGetErrorString(e));
   }
   for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
   return rc;
