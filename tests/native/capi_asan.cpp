@@ -4,7 +4,7 @@
 // into this program by `make -C hmc-stellar-toy-model_amd asan`.
 //
 //   capi_asan cpu   error paths that need no GPU (NULL / bad arguments, no device)
-//   capi_asan gpu   every entry point on small batches: ragged chain counts,
+//   capi_asan gpu   every entry point on small batches (rhmc_energy_device too): ragged chain counts,
 //                   image resize, K = 1 / 3 / 12, all solvers, MH with host and
 //                   device randoms and records, data generation, context churn
 //
@@ -16,6 +16,8 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
+
+#include <hip/hip_runtime_api.h>
 
 #include "rhmc.h"
 
@@ -85,6 +87,8 @@ static void cpu_checks() {
   CHECK(rhmc_gradient(nullptr, &P, q.data(), p.data(), 1, 1, 0) == RHMC_ERR_ARG, "gradient");
   CHECK(rhmc_energy(nullptr, &P, q.data(), p.data(), q.data(), p.data(), 1, 1, 0) == RHMC_ERR_ARG,
         "energy");
+  CHECK(rhmc_energy_device(nullptr, &P, q.data(), p.data(), q.data(), p.data(), 1, 1, 0,
+                           nullptr) == RHMC_ERR_ARG, "energy_device");
   CHECK(rhmc_integrate(nullptr, &P, 1, q.data(), p.data(), 1, 1, 1, 0, nullptr) == RHMC_ERR_ARG,
         "integrate");
   CHECK(rhmc_mh(nullptr, &P, q.data(), 1, 1, 1, 1, 0, nullptr, nullptr, 1, nullptr) ==
@@ -159,6 +163,30 @@ static void gpu_checks() {
             "gradient K=%d", K);
       CHECK(rhmc_energy(ctx, &P, q.data(), p.data(), V.data(), T.data(), n, K, 0) == RHMC_OK,
             "energy K=%d", K);
+      {  // the device-buffer entry point on the context's stream: the same launch, same bits
+        double *dq = nullptr, *dp = nullptr, *dV = nullptr, *dT = nullptr;
+        const size_t sb = q.size() * sizeof(double), eb = (size_t)n * sizeof(double);
+        CHECK(hipMalloc(&dq, sb) == hipSuccess && hipMalloc(&dp, sb) == hipSuccess &&
+                  hipMalloc(&dV, eb) == hipSuccess && hipMalloc(&dT, eb) == hipSuccess,
+              "hipMalloc K=%d", K);
+        CHECK(hipMemcpy(dq, q.data(), sb, hipMemcpyHostToDevice) == hipSuccess &&
+                  hipMemcpy(dp, p.data(), sb, hipMemcpyHostToDevice) == hipSuccess,
+              "H2D K=%d", K);
+        CHECK(rhmc_energy_device(ctx, &P, dq, dp, dV, dT, n, K, 0, nullptr) == RHMC_OK &&
+                  rhmc_ctx_synchronize(ctx) == RHMC_OK, "energy_device K=%d", K);
+        std::vector<double> V2(n), T2(n);
+        CHECK(hipMemcpy(V2.data(), dV, eb, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(T2.data(), dT, eb, hipMemcpyDeviceToHost) == hipSuccess,
+              "D2H K=%d", K);
+        CHECK(std::memcmp(V2.data(), V.data(), eb) == 0 && std::memcmp(T2.data(), T.data(), eb) == 0,
+              "energy_device == energy K=%d", K);
+        CHECK(rhmc_energy_device(ctx, &P, nullptr, dp, dV, dT, n, K, 0, nullptr) == RHMC_ERR_ARG,
+              "energy_device NULL q");
+        (void)hipFree(dq);
+        (void)hipFree(dp);
+        (void)hipFree(dV);
+        (void)hipFree(dT);
+      }
       for (int solver = RHMC_SOLVER_HMC; solver <= RHMC_SOLVER_RHMC_LEAPFROG; ++solver) {
         std::vector<double> qs = q, ps = p;
         CHECK(rhmc_integrate(ctx, &P, solver, qs.data(), ps.data(), n, K, 10, 1, st.data()) ==
