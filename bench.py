@@ -338,7 +338,8 @@ def bench_rj(args, wl, gpu, world, rank):
     t0 = time.perf_counter()
     for i in range(args.steps):
         g.run_RHMC_rj_batched([m.copy() for m in starts], [s + 7 * (i + 1) for s in seeds], **kw)
-        steps += int(np.sum(np.where(g.move_chain == 0, 1, 2))) * leap
+        # move 0: one trajectory; a jump: two, unless its proposal was a dead end
+        steps += int(np.sum(np.where((g.move_chain == 0) | (g.flag_chain != 0), 1, 2))) * leap
     wall = time.perf_counter() - t0
     if world > 1:
         dist.barrier()

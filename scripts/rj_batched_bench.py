@@ -66,7 +66,8 @@ def main():
                           engine=args.engine, n_threads=args.threads, n_pipes=args.pipes)
     wall = time.perf_counter() - t0
     moves = g.move_chain
-    steps = int(np.sum(np.where(moves == 0, 1, 2))) * args.nsteps
+    dead = getattr(g, "flag_chain", np.zeros_like(moves)) != 0
+    steps = int(np.sum(np.where((moves == 0) | dead, 1, 2))) * args.nsteps
     out = {"what": "run_RHMC_rj_batched, big-sim4 geometry (32x32, K0 = 51), P_move "
                    "[0.6, 0.2, 0.2], one seeded stream per chain",
            "engine": args.engine, "pipes": args.pipes, "chains": args.chains, "iterations": args.niter + 1,
