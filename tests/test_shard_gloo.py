@@ -33,10 +33,11 @@ def _worker(rank, world, port, n_total, out_path):
         wl = workloads.make("C2", n_chains=n_total)     # global set, then slice
         local = np.concatenate([wl.q0[lo:hi], wl.p0[lo:hi]], 1)
         t = shard.max_over_ranks(float(rank + 1))
+        tsum = shard.sum_over_ranks(hi - lo)            # bench --mode rj: chain-steps summed
         got = shard.gather_chains(local, n_total)
         dist.barrier()
         if rank == 0:
-            np.savez(out_path, gathered=got, tmax=t)
+            np.savez(out_path, gathered=got, tmax=t, tsum=tsum)
     finally:
         dist.destroy_process_group()
 
@@ -62,3 +63,4 @@ def test_gather_over_gloo(tmp_path, world, n_total):
     wl = workloads.make("C2", n_chains=n_total)
     np.testing.assert_array_equal(z["gathered"], np.concatenate([wl.q0, wl.p0], 1))
     assert float(z["tmax"]) == float(world)
+    assert float(z["tsum"]) == float(n_total)
