@@ -31,6 +31,22 @@ class Legacy {
     gauss_ = 0.0;
   }
 
+  // RandomState.get_state() / set_state() (key, pos, has_gauss, cached_gaussian)
+  void get_state(uint32_t* key, int32_t* pos, int32_t* has_gauss, double* gauss) const {
+    for (int i = 0; i < kN; ++i) key[i] = key_[i];
+    *pos = pos_;
+    *has_gauss = has_gauss_ ? 1 : 0;
+    *gauss = gauss_;
+  }
+  bool set_state(const uint32_t* key, int32_t pos, int32_t has_gauss, double gauss) {
+    if (pos < 0 || pos > kN) return false;
+    for (int i = 0; i < kN; ++i) key_[i] = key[i];
+    pos_ = pos;
+    has_gauss_ = has_gauss != 0;
+    gauss_ = has_gauss_ ? gauss : 0.0;
+    return true;
+  }
+
   uint32_t next32() {
     if (pos_ == kN) generate();
     uint32_t y = key_[pos_++];

@@ -519,7 +519,15 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
   if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
   if (cfg->n_pipes < 0 || cfg->n_pipes > 2) return fail(RHMC_ERR_ARG, "n_pipes must be 0, 1 or 2");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
-  if (n > 0 && (!q || !K || !seeds)) return fail(RHMC_ERR_ARG, "q, K or seeds is NULL");
+  if (n > 0 && (!q || !K)) return fail(RHMC_ERR_ARG, "q or K is NULL");
+  if (cfg->use_states != 0 && cfg->use_states != 1)
+    return fail(RHMC_ERR_ARG, "use_states must be 0 or 1");
+  if (n > 0 && cfg->use_states && !cfg->states)
+    return fail(RHMC_ERR_ARG, "use_states without states");
+  if (n > 0 && !cfg->use_states && !seeds) return fail(RHMC_ERR_ARG, "seeds is NULL");
+  for (int64_t c = 0; cfg->use_states && c < n; ++c)
+    if (cfg->states[c].pos < 0 || cfg->states[c].pos > 624)
+      return fail(RHMC_ERR_ARG, "states[c].pos must be in [0, 624]");
   if (cfg->n_iter < 0 || cfg->n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter or n_steps < 0");
   if (cfg->N_max < 1 || cfg->N_max > 256) return fail(RHMC_ERR_ARG, "N_max must be in [1, 256]");
   if (cfg->rows < 3 || cfg->cols < 3) return fail(RHMC_ERR_ARG, "rows / cols < 3");
@@ -571,7 +579,12 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
   for (int64_t c = 0; c < n; ++c) {
     all[c] = c;
     Chain& h = R.ch[c];
-    h.rng.seed(seeds[c]);
+    if (cfg->use_states) {
+      const rhmc_np_state& st = cfg->states[rec_off + c];
+      h.rng.set_state(st.key, st.pos, st.has_gauss, st.gauss);
+    } else {
+      h.rng.seed(seeds[c]);
+    }
     h.K = K[c];
     h.q.assign(q + c * W, q + c * W + 3 * (int64_t)K[c]);
   }
@@ -703,6 +716,10 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
     std::fill(q + c * W, q + (c + 1) * W, 0.);
     std::copy(h.q.begin(), h.q.end(), q + c * W);
     K[c] = h.K;
+    if (cfg->states) {
+      rhmc_np_state& st = cfg->states[rec_off + c];
+      h.rng.get_state(st.key, &st.pos, &st.has_gauss, &st.gauss);
+    }
   }
   return 0;
 }
@@ -900,7 +917,7 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
       int rc1 = 0;
       std::string err1;
       std::thread t([&] {
-        rc1 = run(phys, nullptr, P, cfg, q + h * W, K + h, seeds + h, n - h, rec, n, h,
+        rc1 = run(phys, nullptr, P, cfg, q + h * W, K + h, seeds ? seeds + h : nullptr, n - h, rec, n, h,
                   std::max(1, nt / 2), phase1);
         if (rc1) err1 = g_err;
       });
@@ -965,7 +982,7 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
           err1 = "hipSetDevice failed";
           return;
         }
-        rc1 = run(&phys1, &st1, P, cfg, q + h * W, K + h, seeds + h, n - h, rec, n, h, nt1,
+        rc1 = run(&phys1, &st1, P, cfg, q + h * W, K + h, seeds ? seeds + h : nullptr, n - h, rec, n, h, nt1,
                   phase1);
         if (rc1) err1 = g_err;
       });

@@ -37,11 +37,36 @@ class RjConfig(ctypes.Structure):
                 ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
                 ("n_threads", ctypes.c_int32), ("n_g_ff2", ctypes.c_int32),
                 ("n_beta", ctypes.c_int32), ("n_pipes", ctypes.c_int32),
-                ("reserved", ctypes.c_int32),
+                ("use_states", ctypes.c_int32), ("reserved", ctypes.c_int32),
                 ("P_move", ctypes.c_double * 3), ("fmin", ctypes.c_double),
                 ("fmax", ctypes.c_double), ("K_split", ctypes.c_double),
                 ("beta_a", ctypes.c_double), ("beta_b", ctypes.c_double),
-                ("schedule_g_ff2", ctypes.c_void_p), ("schedule_beta", ctypes.c_void_p)]
+                ("schedule_g_ff2", ctypes.c_void_p), ("schedule_beta", ctypes.c_void_p),
+                ("states", ctypes.c_void_p)]
+
+
+# rhmc_np_state: one chain's RandomState.get_state() (key, pos, has_gauss, gauss)
+STATE_DTYPE = np.dtype([("key", "<u4", 624), ("pos", "<i4"), ("has_gauss", "<i4"),
+                        ("gauss", "<f8")])
+
+
+def states_from(random_states):
+    """rhmc_np_state rows of a list of numpy.random.RandomState objects."""
+    out = np.zeros(len(random_states), dtype=STATE_DTYPE)
+    for i, rs in enumerate(random_states):
+        name, key, pos, has_gauss, gauss = rs.get_state()
+        if name != "MT19937":
+            raise ValueError("not an MT19937 RandomState")
+        out[i] = (np.asarray(key, dtype=np.uint32), pos, has_gauss, gauss)
+    return out
+
+
+def random_state(row):
+    """A numpy.random.RandomState continuing one rhmc_np_state row's stream."""
+    rs = np.random.RandomState()
+    rs.set_state(("MT19937", np.array(row["key"], dtype=np.uint32), int(row["pos"]),
+                  int(row["has_gauss"]), float(row["gauss"])))
+    return rs
 
 
 class RjRecord(ctypes.Structure):
@@ -100,13 +125,16 @@ def np_draws(seed, kind, n, a=0., b=0.):
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0, n_pipes=0):
+        n_threads=0, n_pipes=0, states=None):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
     vectors.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
-    -> None, in place; for stand-ins).  Returns (q list, record dict)."""
+    -> None, in place; for stand-ins).  states: None (streams from the seeds)
+    or an array of STATE_DTYPE rows to start from (then seeds may be None).
+    Returns (q list, record dict); record["states"] holds every chain's stream
+    at the end (pass it back as `states` to resume)."""
     n = len(q_models)
-    if len(seeds) != n:
+    if states is None and (seeds is None or len(seeds) != n):
         raise ValueError("one seed per chain")
     W = 3 * int(N_max)
     q = np.zeros((n, W))
@@ -117,10 +145,17 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
             raise ValueError("chain %d: %d values for N_max %d" % (c, qm.size, N_max))
         q[c, :qm.size] = qm
         K[c] = qm.size // 3
-    sd = np.asarray(seeds, dtype=np.int64)
-    if sd.size and (sd.min() < 0 or sd.max() > 2 ** 32 - 1):
-        raise ValueError("seeds must be in [0, 2**32)")
-    sd = sd.astype(np.uint32)
+    if states is not None:
+        st = np.ascontiguousarray(np.array(states, dtype=STATE_DTYPE))
+        if st.shape != (n,):
+            raise ValueError("one state per chain")
+        sd = np.zeros(n, dtype=np.uint32)
+    else:
+        st = np.zeros(n, dtype=STATE_DTYPE)
+        sd = np.asarray(seeds, dtype=np.int64)
+        if sd.size and (sd.min() < 0 or sd.max() > 2 ** 32 - 1):
+            raise ValueError("seeds must be in [0, 2**32)")
+        sd = sd.astype(np.uint32)
     keep = []
 
     def arr(a):
@@ -133,15 +168,15 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     sb, nb = arr(schedule_beta)
     pm = (ctypes.c_double * 3)(*[float(v) for v in P_move])
     cfg = RjConfig(int(n_iter), int(n_steps), int(N_max), int(f_pos), int(rows), int(cols),
-                   int(n_threads), ng, nb, int(n_pipes), 0, pm, float(fmin), float(fmax),
-                   float(K_split),
-                   float(beta_a), float(beta_b), sg, sb)
+                   int(n_threads), ng, nb, int(n_pipes), int(states is not None), 0, pm,
+                   float(fmin), float(fmax), float(K_split), float(beta_a), float(beta_b), sg,
+                   sb, st.ctypes.data if n else None)
     rows_n = int(n_iter) + 1
     rec = {"q_chain": np.zeros((rows_n, n, W)), "p_chain": np.zeros((rows_n, n, W)),
            "E_chain": np.zeros((rows_n, n)), "V_chain": np.zeros((rows_n, n)),
            "T_chain": np.zeros((rows_n, n)), "accept": np.zeros((rows_n, n), np.int32),
            "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),
-           "flags": np.zeros((rows_n, n), np.int32), "phase_s": np.zeros(7)}
+           "flags": np.zeros((rows_n, n), np.int32), "phase_s": np.zeros(7), "states": st}
     r = RjRecord(*[rec[k].ctypes.data for k in ("q_chain", "p_chain", "E_chain", "V_chain",
                                                   "T_chain", "accept", "move", "n_stars",
                                                   "flags", "phase_s")])

@@ -682,7 +682,7 @@ class multi_gym(base_class):
     def run_RHMC_rj_batched(self, q_models_0, seeds, f_pos=True, delta=1e-6, Niter=100,
                             Nsteps=100, dt=1e-1, counter_max=1000, N_max=50,
                             P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None,
-                            engine="native", n_threads=0, n_pipes=0):
+                            engine="native", n_threads=0, n_pipes=0, rng_states=None):
         """Many independent chains of run_RHMC WITH the reversible-jump moves
         (sampler_RHMC.py:937-1198; birth_death_move :1200-1270, split_merge_move
         :1273-1445), each chain at its own, changing, star count.  Chain c is
@@ -694,8 +694,9 @@ class multi_gym(base_class):
         — runs batched over the chains, one launch per distinct star count
         (chains grouped by K, so the kernels see ordinary fixed-K batches).
 
-        q_models_0: a list of [K_c, 3] (mag, x, y) arrays.  Returns a list of
-        the chains' final q; sets q_chain / p_chain [Niter+1, n, 3 N_max],
+        q_models_0: a list of [K_c, 3] (mag, x, y) arrays, or of the flat
+        flux-count q vectors a run returned (taken as they are: a resume).
+        Returns a list of the chains' final q; sets q_chain / p_chain [Niter+1, n, 3 N_max],
         E/V/T_chain, A_chain, move_chain, N_chain [Niter+1, n] (iteration-major,
         like run_RHMC_batched).
 
@@ -706,17 +707,24 @@ class multi_gym(base_class):
         proposal was a dead end (see the header); n_pipes = 2 (the default
         from 1024 chains) runs the chains in two halves whose host and GPU
         phases overlap, 1 keeps the engine batches of the NumPy loop;
-        engine="python" is the NumPy loop below (the reference's own draws
-        through np.random)."""
+        rng_states (native only): the chains' streams to start from instead of
+        the seeds — a list of numpy RandomState objects or the rj_rng_states
+        array an earlier run left (run it from that run's final q: the draws of
+        one uninterrupted run); engine="python" is the NumPy loop below (the
+        reference's own draws through np.random)."""
         n = len(q_models_0)
-        if len(seeds) != n:
-            raise ValueError("one seed per chain")
         if engine == "native":
+            if rng_states is None and (seeds is None or len(seeds) != n):
+                raise ValueError("one seed per chain")
             return self._rj_native(q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt,
                                    counter_max, N_max, P_move, schedule_g_ff2, schedule_beta,
-                                   n_threads, n_pipes)
+                                   n_threads, n_pipes, rng_states)
         if engine != "python":
             raise ValueError("engine must be 'native' or 'python'")
+        if rng_states is not None:
+            raise ValueError("rng_states needs engine='native'")
+        if len(seeds) != n:
+            raise ValueError("one seed per chain")
         self.dt, self.Niter, self.Nsteps = dt, Niter, Nsteps
         self.P_move, self.N_max = P_move, N_max
         n_it = Niter + 1
@@ -728,7 +736,7 @@ class multi_gym(base_class):
         self.N_chain = np.zeros((n_it, n), dtype=int)
         saved = np.random.get_state()
         streams = [np.random.RandomState(s) for s in seeds]   # == np.random.seed(s)
-        q = [self.format_q(np.array(m, dtype=np.float64).copy()) for m in q_models_0]
+        q = [self._start_q(m) for m in q_models_0]
         p = [None] * n
         move = [0] * n
         grow = [False] * n
@@ -824,8 +832,19 @@ class multi_gym(base_class):
         self.Nobjs = self.d = None
         return q
 
+    def _start_q(self, m):
+        """A chain's start for run_RHMC_rj_batched: [K, 3] (mag, x, y) rows are
+        formatted (format_q); a flat q (what the run returns) is used as is."""
+        m = np.asarray(m, dtype=np.float64)
+        if m.ndim == 1:
+            if m.size % 3:
+                raise ValueError("a flat q holds 3 values per star")
+            return m.copy()
+        return self._format_q_fast(m)
+
     def _rj_native(self, q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt, counter_max, N_max,
-                   P_move, schedule_g_ff2, schedule_beta, n_threads, n_pipes=0):
+                   P_move, schedule_g_ff2, schedule_beta, n_threads, n_pipes=0,
+                   rng_states=None):
         """run_RHMC_rj_batched through librhmc_rj.so (rhmc_rj_run)."""
         from . import rj_native
         self._check_geometry()
@@ -834,7 +853,7 @@ class multi_gym(base_class):
         jumps = P_move[1] != 0 or P_move[2] != 0
         if jumps and (self.alpha is None or self.fmin is None or self.fmax is None):
             assert False                                  # :1205-1207 (prior required)
-        q0 = [self._format_q_fast(m) for m in q_models_0]
+        q0 = [self._start_q(m) for m in q_models_0]
         P = self._params(delta, counter_max, for_energy=True)
         import time
         t0 = time.perf_counter()
@@ -843,7 +862,9 @@ class multi_gym(base_class):
             self.num_rows, self.num_cols, self.fmin if jumps else 1., self.fmax if jumps else 1.,
             self.K_split, self.beta_a, self.beta_b, schedule_g_ff2=schedule_g_ff2,
             schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads,
-            n_pipes=n_pipes)
+            n_pipes=n_pipes, states=(None if rng_states is None else
+                                     rng_states if isinstance(rng_states, np.ndarray)
+                                     else rj_native.states_from(rng_states)))
         self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
         for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):
@@ -855,6 +876,7 @@ class multi_gym(base_class):
         self.move_chain = rec["move"].astype(int)
         self.N_chain = rec["n_stars"].astype(int)
         self.flag_chain = rec["flags"]
+        self.rj_rng_states = rec["states"]     # every chain's stream at the end (resume)
         self.rj_phase_s = dict(zip(("draws", "V0", "steps1", "proposals", "steps2", "V1",
                                     "accept"), rec["phase_s"]))
         self.Nobjs = self.d = None

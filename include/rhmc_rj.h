@@ -64,6 +64,15 @@ typedef struct rhmc_rj_physics {
                int32_t n_steps);
 } rhmc_rj_physics;
 
+/* One chain's NumPy legacy stream: RandomState.get_state() = ('MT19937', key,
+ * pos, has_gauss, cached_gaussian).  2512 bytes. */
+typedef struct rhmc_np_state {
+  uint32_t key[624];
+  int32_t pos;
+  int32_t has_gauss;
+  double gauss;
+} rhmc_np_state;
+
 typedef struct rhmc_rj_config {
   int32_t n_iter;        /* Niter: iterations 0 .. n_iter (n_iter + 1 records)      */
   int32_t n_steps;       /* Nsteps per trajectory                                    */
@@ -77,6 +86,9 @@ typedef struct rhmc_rj_config {
                             of multi_gym.run_RHMC_rj_batched); 2: the chains in two
                             halves on two host threads, so one half's host work
                             overlaps the other's GPU work; 0: 2 from 1024 chains    */
+  int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
+                            seeds[c] (a checkpoint of an earlier run, or any
+                            RandomState's get_state(): continue its stream)        */
   int32_t reserved;      /* must be 0                                                */
   double P_move[3];      /* within / birth-death / split-merge probabilities         */
   double fmin, fmax;     /* power-law flux prior range, counts (:1221)               */
@@ -84,6 +96,10 @@ typedef struct rhmc_rj_config {
   double beta_a, beta_b; /* split fraction F ~ Beta(beta_a, beta_b) (:1302)          */
   const double* schedule_g_ff2;  /* iteration l: g_ff2 = s[min(l, n - 1)] (:1010-1013) */
   const double* schedule_beta;   /* likewise beta (:1014-1016)                        */
+  rhmc_np_state* states;         /* nullable [n]: read when use_states, and written with
+                                    every chain's stream at the end of the run (resume a
+                                    run from its q, K and states: the same draws as one
+                                    uninterrupted run)                                 */
 } rhmc_rj_config;
 
 /* Per-iteration records, row l = the state at the START of iteration l

@@ -174,6 +174,51 @@ int main(int argc, char** argv) {
         CHECK(rc == 0, "run");
         for (int i = 0; i < n; ++i) CHECK(K[i] >= 1 && K[i] <= c.N_max, "star count range");
       }
+  // checkpoint: rows 0..11 == rows 0..5 + (resume from the states) rows 0..5, two pipes
+  {
+    const int m = 23;
+    rhmc_rj_config c = config(11, 6, 0.4, 0.3, 0.3);
+    c.n_pipes = 2;
+    const int W = 3 * c.N_max;
+    std::vector<double> q0((size_t)m * W, 0.);
+    std::vector<int32_t> K0(m);
+    std::vector<uint32_t> seeds(m);
+    for (int i = 0; i < m; ++i) {
+      K0[i] = 1 + i % 5;
+      seeds[i] = 900u + (uint32_t)i;
+      for (int k = 0; k < K0[i]; ++k) {
+        q0[(size_t)i * W + 3 * k] = 600. + 250. * k;
+        q0[(size_t)i * W + 3 * k + 1] = 6. + 3. * k;
+        q0[(size_t)i * W + 3 * k + 2] = 22. - 2. * k;
+      }
+    }
+    std::vector<double> qa = q0, qb = q0;
+    std::vector<int32_t> Ka = K0, Kb = K0;
+    std::vector<rhmc_np_state> sa(m), sb(m);
+    c.states = sa.data();
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, qa.data(), Ka.data(), seeds.data(), m, nullptr) == 0,
+          "full run");
+    c.n_iter = 5;
+    c.states = sb.data();
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, qb.data(), Kb.data(), seeds.data(), m, nullptr) == 0,
+          "first half");
+    c.use_states = 1;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, qb.data(), Kb.data(), nullptr, m, nullptr) == 0,
+          "resumed half");
+    CHECK(std::memcmp(qa.data(), qb.data(), qa.size() * sizeof(double)) == 0, "resume q");
+    CHECK(std::memcmp(Ka.data(), Kb.data(), Ka.size() * sizeof(int32_t)) == 0, "resume K");
+    CHECK(std::memcmp(sa.data(), sb.data(), sa.size() * sizeof(rhmc_np_state)) == 0,
+          "resume states");
+    c.states = nullptr;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, qb.data(), Kb.data(), seeds.data(), m, nullptr) ==
+              RHMC_ERR_ARG,
+          "use_states without states");
+    c.states = sb.data();
+    sb[3].pos = 625;
+    CHECK(rhmc_rj_run_physics(&phys, &P, &c, qb.data(), Kb.data(), seeds.data(), m, nullptr) ==
+              RHMC_ERR_ARG,
+          "state pos range");
+  }
   // errors
   {
     rhmc_rj_config c = config(2, 4, 0.5, 0.25, 0.25);

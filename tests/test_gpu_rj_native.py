@@ -137,6 +137,40 @@ def test_native_two_pipes_equal_one(gpu_lib):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
 
 
+def test_native_checkpoint_resume_on_the_engine(gpu_lib):
+    """A run of Niter = 11 (rows 0..11) == a run of Niter = 5 and a resume from
+    its final q and rj_rng_states for Niter = 5 more: the same engine batches
+    in the same order, so every record is bit-identical; and rng_states taken
+    from fresh RandomState(seed) objects is the seeded run."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+
+    def make():
+        g = _gym(par)
+        g.D = z[name + "/D"]
+        return g
+    rs = np.random.RandomState(13)
+    starts = _starts(z[name + "/q_model"], 48, rs)
+    seeds = list(range(900, 948))
+    kw = dict(f_pos=True, delta=1e-6, Nsteps=6, dt=0.05, N_max=12, P_move=[0.4, 0.3, 0.3],
+              n_pipes=2)
+    a, b, c = make(), make(), make()
+    qa = a.run_RHMC_rj_batched([m.copy() for m in starts], seeds, Niter=11, **kw)
+    qb = b.run_RHMC_rj_batched([m.copy() for m in starts], None, Niter=5, **kw,
+                               rng_states=[np.random.RandomState(s) for s in seeds])
+    rec_b = {k: getattr(b, k).copy() for k in ("move_chain", "N_chain", "A_chain",
+                                                 "flag_chain", "q_chain", "E_chain")}
+    qc = c.run_RHMC_rj_batched(qb, None, Niter=5, **kw, rng_states=b.rj_rng_states)
+    for k, v in rec_b.items():
+        np.testing.assert_array_equal(getattr(a, k),
+                                      np.concatenate([v, getattr(c, k)]), err_msg=k)
+    for x, y in zip(qa, qc):
+        np.testing.assert_array_equal(x, y)
+    assert np.array_equal(a.rj_rng_states, c.rj_rng_states)
+    assert (a.move_chain[a.A_chain] > 0).any()
+
+
 @pytest.mark.parametrize("golden,name", [("rj", "rj_bd"), ("rj", "rj_sm"), ("rj", "rj_all"),
                                          ("mh", "mh1"), ("mh", "mh3"), ("mh_sched", "g1"),
                                          ("mh_sched", "g3"), ("mh_sched", "g3vc")])

@@ -188,3 +188,93 @@ def test_argument_errors(rj):
         def bad(q, fp):
             raise RuntimeError("boom")
         rj.run(P, q, [1], **base, physics=(bad, phys[1]))
+
+
+def test_states_round_trip_and_continue_a_random_state(rj):
+    """rhmc_np_state rows are RandomState.get_state(): a state taken after some
+    draws (a cached gaussian included) continues that stream inside the
+    driver, and the states a run leaves are the streams' true positions."""
+    rs = [np.random.RandomState(s) for s in (5, 6, 7)]
+    rs[0].randn(3)                                  # has_gauss = 1
+    rs[1].random_sample(700)                        # past a twist
+    st = rj.states_from(rs)
+    assert st["has_gauss"][0] == 1 and st["pos"][1] != 624
+    for r, row in zip(rs, st):
+        a, b = r.get_state(), rj.random_state(row).get_state()
+        assert np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+    # the driver continuing those streams == the driver started from the
+    # seeds after the same draws: compare against a fresh run of each
+    starts = STARTS[:3]
+    kw = dict(f_pos=True, Niter=6, Nsteps=2, dt=0.05, N_max=8, P_move=[0.4, 0.3, 0.3])
+    g = _gym()
+    qms = [g.format_q(m.copy()) for m in starts]
+    P = g._params(for_energy=True)
+    phys = (lambda q, fp: g.V(q), lambda q, p, ns: _inplace(g, q, p, ns))
+    base = dict(n_iter=6, n_steps=2, N_max=8, P_move=kw["P_move"], f_pos=1, rows=g.num_rows,
+                cols=g.num_cols, fmin=g.fmin, fmax=g.fmax, K_split=g.K_split, beta_a=g.beta_a,
+                beta_b=g.beta_b, physics=phys)
+    fresh = rj.states_from([np.random.RandomState(s) for s in (5, 6, 7)])
+    _, r_seed = rj.run(P, qms, [5, 6, 7], **base)
+    _, r_state = rj.run(P, qms, None, **base, states=fresh)
+    for k in r_seed:
+        if k != "phase_s":
+            assert np.array_equal(r_seed[k], r_state[k]), k
+    # the streams moved on, and a drawn-from stream starts elsewhere
+    assert (r_seed["states"]["pos"] != 624).any() or \
+        not np.array_equal(r_seed["states"]["key"], fresh["key"])
+    _, r_used = rj.run(P, qms, None, **base, states=st)
+    assert not np.array_equal(r_used["move"], r_seed["move"]) or \
+        not np.array_equal(r_used["q_chain"], r_seed["q_chain"])
+
+
+def _inplace(g, q, p, ns):
+    qq, pp = g.RHMC_steps(q, p, ns)
+    q[:] = qq
+    p[:] = pp
+
+
+@pytest.mark.parametrize("n_pipes", [1, 2])
+def test_checkpoint_resume_is_one_run(rj, n_pipes):
+    """One run == a run, then a resume from its final q, K and states:
+    bit-identical records (the checkpoint of the
+    reference's long runs, which restart np.random from a saved state)."""
+    starts = [np.array([[18.5, 16., 16.]])] * 6 + STARTS * 4
+    seeds = list(range(40, 40 + len(starts)))
+    kw = dict(f_pos=True, Niter=14, Nsteps=2, dt=0.05, N_max=7, P_move=[0.3, 0.35, 0.35])
+    q_full, r_full = _native(rj, _gym(), starts, seeds, kw, n_threads=3, n_pipes=n_pipes)
+    g = _gym()
+    P = g._params(for_energy=True)
+    base = dict(n_steps=2, N_max=7, P_move=kw["P_move"], f_pos=1, rows=g.num_rows,
+                cols=g.num_cols, fmin=g.fmin, fmax=g.fmax, K_split=g.K_split, beta_a=g.beta_a,
+                beta_b=g.beta_b, n_threads=5, n_pipes=n_pipes,
+                physics=(lambda q, fp: g.V(q), lambda q, p, ns: _inplace(g, q, p, ns)))
+    qms = [g.format_q(m.copy()) for m in starts]
+    q_a, r_a = rj.run(P, qms, seeds, n_iter=9, **base)
+    # a run of n_iter records n_iter + 1 iterations (rows 0..n_iter, as the
+    # reference): 10 + 5 rows == the 15 of Niter=14
+    q_b, r_b = rj.run(P, q_a, None, n_iter=4, **base, states=r_a["states"])
+    assert all(np.array_equal(a, b) for a, b in zip(q_full, q_b))
+    assert np.array_equal(r_full["states"], r_b["states"])
+    for k in r_full:
+        if k in ("phase_s", "states"):
+            continue
+        assert np.array_equal(r_full[k], np.concatenate([r_a[k], r_b[k]])), k
+    assert r_full["flags"].any()                    # the resume crossed dead ends too
+
+
+def test_state_errors(rj):
+    from rhmc_amd import capi
+    g = _gym()
+    P = g._params(for_energy=True)
+    phys = (lambda q, fp: np.zeros(len(q)), lambda q, p, ns: None)
+    base = dict(n_iter=2, n_steps=1, N_max=4, P_move=[0.5, 0.25, 0.25], f_pos=1, rows=32,
+                cols=32, fmin=g.fmin, fmax=g.fmax, K_split=1., beta_a=2., beta_b=2., physics=phys)
+    q = [g.format_q(STARTS[1].copy())]
+    with pytest.raises(ValueError, match="one state"):
+        rj.run(P, q, None, **base, states=rj.states_from([np.random.RandomState(1)] * 2))
+    bad = rj.states_from([np.random.RandomState(1)])
+    bad["pos"] = 700
+    with pytest.raises(capi.RhmcError, match="pos"):
+        rj.run(P, q, None, **base, states=bad)
+    with pytest.raises(ValueError, match="seed"):
+        rj.run(P, q, None, **base)
