@@ -20,6 +20,7 @@
 #include "rhmc_rj.h"
 
 #include <algorithm>
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -37,6 +38,8 @@
 #include "np_legacy.hpp"
 
 namespace {
+
+constexpr int kMaxPipes = 4;  // rhmc_rj_config::n_pipes
 
 thread_local std::string g_err;
 
@@ -517,7 +520,8 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
           const uint32_t* seeds, int64_t n) {
   if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
   if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
-  if (cfg->n_pipes < 0 || cfg->n_pipes > 2) return fail(RHMC_ERR_ARG, "n_pipes must be 0, 1 or 2");
+  if (cfg->n_pipes < 0 || cfg->n_pipes > kMaxPipes)
+    return fail(RHMC_ERR_ARG, "n_pipes must be in [0, 4]");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
   if (n > 0 && (!q || !K)) return fail(RHMC_ERR_ARG, "q or K is NULL");
   if (cfg->use_states != 0 && cfg->use_states != 1)
@@ -729,6 +733,7 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
 // (rhmc_leapfrog_device), so that small groups fill the GPU together instead
 // of one after the other
 constexpr int kStreams = 4;
+static_assert(kStreams >= kMaxPipes, "a stream per pipe at least");
 
 // The streams live for the process, kStreams per device, created on first use
 // and warmed by one small copy each: the first dispatch to a new HIP stream
@@ -899,6 +904,48 @@ int ctx_energy_staged(void* user, const rhmc_params* P, int32_t G, const int32_t
   return rc;
 }
 
+// Split n chains into `pipes` contiguous parts run concurrently, part i on
+// its own host thread (part 0 on the caller's) with its share of the nt pool
+// threads: body(i, first chain, count, threads, phase[7]) -> rc.  The first
+// failing part's error is the one reported.
+template <class Body>
+int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
+  if (pipes <= 1) return body(0, 0, n, nt, phase);
+  std::vector<int64_t> first((size_t)pipes + 1);
+  for (int i = 0; i <= pipes; ++i) first[i] = n * i / pipes;
+  std::vector<int> threads((size_t)pipes);
+  for (int i = 0; i < pipes; ++i) threads[i] = std::max(1, nt * (i + 1) / pipes - nt * i / pipes);
+  std::vector<std::array<double, 7>> ph((size_t)pipes);
+  std::vector<int> rcs((size_t)pipes, 0);
+  std::vector<std::string> errs((size_t)pipes);
+  std::vector<std::thread> ts;
+  for (int i = 1; i < pipes; ++i)
+    ts.emplace_back([&, i] {
+      ph[i].fill(0.);
+      rcs[i] = body(i, first[i], first[i + 1] - first[i], threads[i], ph[i].data());
+      if (rcs[i]) errs[i] = g_err;
+    });
+  ph[0].fill(0.);
+  rcs[0] = body(0, first[0], first[1] - first[0], threads[0], ph[0].data());
+  if (rcs[0]) errs[0] = g_err;
+  for (auto& t : ts) t.join();
+  for (int i = 0; i < pipes; ++i)
+    for (int k = 0; k < 7; ++k) phase[k] += ph[i][k];
+  for (int i = 0; i < pipes; ++i)
+    if (rcs[i]) {
+      g_err = errs[i];
+      return rcs[i];
+    }
+  return 0;
+}
+
+int pipes_for(const rhmc_rj_config* cfg, int64_t n) {
+  // default: measured at big-sim4 geometry (profiles/r04_pipes/): 2 pipes
+  // from 1,024 chains, 4 from 16,384 (1.39x one pipe there; 3 and 4 lose at 4,096)
+  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 16384 ? 4 : n >= 1024 ? 2 : 1);
+  return (int)std::max<int64_t>(1, std::min<int64_t>(pipes, n));
+}
+
 }  // namespace
 
 extern "C" {
@@ -910,27 +957,13 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};
     const int nt = host_threads(cfg);
-    int rc = 0;
-    if (cfg->n_pipes == 2 && n >= 2) {   // the callbacks are then called from two threads
-      const int64_t h = n / 2, W = 3 * (int64_t)cfg->N_max;
-      double phase1[7] = {0, 0, 0, 0, 0, 0, 0};
-      int rc1 = 0;
-      std::string err1;
-      std::thread t([&] {
-        rc1 = run(phys, nullptr, P, cfg, q + h * W, K + h, seeds ? seeds + h : nullptr, n - h, rec, n, h,
-                  std::max(1, nt / 2), phase1);
-        if (rc1) err1 = g_err;
-      });
-      rc = run(phys, nullptr, P, cfg, q, K, seeds, h, rec, n, 0, std::max(1, nt - nt / 2), phase);
-      t.join();
-      for (int i = 0; i < 7; ++i) phase[i] += phase1[i];
-      if (rc == 0 && rc1 != 0) {
-        g_err = err1;
-        rc = rc1;
-      }
-    } else {
-      rc = run(phys, nullptr, P, cfg, q, K, seeds, n, rec, n, 0, nt, phase);
-    }
+    // with pipes > 1 the callbacks are called from that many threads at once
+    const int64_t W = 3 * (int64_t)cfg->N_max;
+    int rc = run_pipes(cfg->n_pipes > 1 ? pipes_for(cfg, n) : 1, n, nt, phase,
+                       [&](int, int64_t f, int64_t m, int t, double* ph) {
+                         return run(phys, nullptr, P, cfg, q + f * W, K + f,
+                                    seeds ? seeds + f : nullptr, m, rec, n, f, t, ph);
+                       });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
   } catch (const std::exception& e) {
@@ -943,57 +976,34 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   try {
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
-    CtxEngine E0, E1;
-    E0.ctx = E1.ctx = ctx;
-    if (int rc = engine_init(E0)) return rc;
+    CtxEngine E[kMaxPipes];
+    for (auto& e : E) e.ctx = ctx;
+    if (int rc = engine_init(E[0])) return rc;
     if (n > 0)
-      if (int rc = engine_warm(E0, P, K[0])) return rc;
-    int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 1024 ? 2 : 1);
-    if (pipes > 2 || n < 2) pipes = std::min(pipes, n < 2 ? 1 : 2);
+      if (int rc = engine_warm(E[0], P, K[0])) return rc;
+    const int pipes = pipes_for(cfg, n);
     const int nt = host_threads(cfg);
-    rhmc_rj_physics phys0{&E0, ctx_energy, ctx_steps}, phys1{&E1, ctx_energy, ctx_steps};
-    Run::Staged st0, st1;
-    st0.user = &E0;
-    st1.user = &E1;
-    for (Run::Staged* st : {&st0, &st1}) {
-      st->buffer = ctx_buffer;
-      st->launch = ctx_launch;
-      st->energy = ctx_energy_staged;
+    // pipe i takes streams i, i + pipes, ... (the HIP calls of the *_device
+    // entry points touch no shared context state)
+    for (int i = 0; i < pipes; ++i) {
+      E[i].dev = E[0].dev;
+      E[i].ns = 0;
+      for (int j = i; j < kStreams; j += pipes) E[i].s[E[i].ns++] = E[0].s[j];
     }
+    const int64_t W = 3 * (int64_t)cfg->N_max;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};
-    int rc = 0;
-    if (pipes == 1) {
-      rc = run(&phys0, &st0, P, cfg, q, K, seeds, n, rec, n, 0, nt, phase);
-    } else {
-      // two halves, two host threads, two streams each (the HIP calls of the
-      // *_device entry points touch no shared context state)
-      const int64_t h = n / 2, W = 3 * (int64_t)cfg->N_max;
-      for (int i = 0; i < kStreams; ++i) E1.s[i] = E0.s[i];
-      E0.ns = E1.ns = kStreams / 2;
-      for (int i = 0; i < kStreams / 2; ++i) E1.s[i] = E0.s[kStreams / 2 + i];
-      const int nt1 = std::max(1, nt / 2), nt0 = std::max(1, nt - nt1);
-      double phase1[7] = {0, 0, 0, 0, 0, 0, 0};
-      int rc1 = 0;
-      std::string err1;
-      std::thread t([&] {
-        E1.dev = E0.dev;
-        if (hipSetDevice(E1.dev) != hipSuccess) {
-          rc1 = RHMC_ERR_HIP;
-          err1 = "hipSetDevice failed";
-          return;
-        }
-        rc1 = run(&phys1, &st1, P, cfg, q + h * W, K + h, seeds ? seeds + h : nullptr, n - h, rec, n, h, nt1,
-                  phase1);
-        if (rc1) err1 = g_err;
-      });
-      rc = run(&phys0, &st0, P, cfg, q, K, seeds, h, rec, n, 0, nt0, phase);
-      t.join();
-      for (int i = 0; i < 7; ++i) phase[i] += phase1[i];
-      if (rc == 0 && rc1 != 0) {
-        g_err = err1;
-        rc = rc1;
-      }
-    }
+    const int rc = run_pipes(pipes, n, nt, phase, [&](int i, int64_t f, int64_t m, int t,
+                                                      double* ph) {
+      if (i > 0 && hipSetDevice(E[i].dev) != hipSuccess) return fail(RHMC_ERR_HIP, "hipSetDevice failed");
+      rhmc_rj_physics phys{&E[i], ctx_energy, ctx_steps};
+      Run::Staged st;
+      st.user = &E[i];
+      st.buffer = ctx_buffer;
+      st.launch = ctx_launch;
+      st.energy = ctx_energy_staged;
+      return run(&phys, &st, P, cfg, q + f * W, K + f, seeds ? seeds + f : nullptr, m, rec, n, f,
+                 t, ph);
+    });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
   } catch (const std::exception& e) {

@@ -101,7 +101,7 @@ struct Rec {
 };
 
 // gpu mode: rhmc_rj_run on a real context (the staged, stream-concurrent
-// engine path, one and two pipes) on a synthetic 32x32 image
+// engine path, one, two and four pipes) on a synthetic 32x32 image
 static void gpu_mode(const rhmc_params& P) {
   std::vector<double> D(32 * 32);
   for (int i = 0; i < 32 * 32; ++i) D[i] = 25. + (i % 7);
@@ -109,7 +109,7 @@ static void gpu_mode(const rhmc_params& P) {
   CHECK(rhmc_ctx_create(0, D.data(), 32, 32, &ctx) == 0, "ctx create");
   if (!ctx) return;
   const int n = 45;
-  for (int pipes = 1; pipes <= 2; ++pipes) {
+  for (int pipes = 1; pipes <= 4; pipes *= 2) {
     rhmc_rj_config c = config(6, 16, 0.4, 0.3, 0.3);
     c.n_pipes = pipes;
     const int W = 3 * c.N_max;
@@ -142,7 +142,7 @@ int main(int argc, char** argv) {
   rhmc_rj_physics phys{nullptr, fake_energy, fake_steps};
   const int n = 37;
   for (int mix = 0; mix < 3; ++mix)
-    for (int pipes = 1; pipes <= 2; ++pipes)
+    for (int pipes = 1; pipes <= 4; ++pipes)
       for (int with_rec = 0; with_rec < 2; ++with_rec) {
         rhmc_rj_config c = mix == 0 ? config(15, 6, 0.4, 0.3, 0.3)
                            : mix == 1 ? config(15, 6, 0.2, 0.8, 0.0)
@@ -174,11 +174,11 @@ int main(int argc, char** argv) {
         CHECK(rc == 0, "run");
         for (int i = 0; i < n; ++i) CHECK(K[i] >= 1 && K[i] <= c.N_max, "star count range");
       }
-  // checkpoint: rows 0..11 == rows 0..5 + (resume from the states) rows 0..5, two pipes
+  // checkpoint: rows 0..11 == rows 0..5 + (resume from the states) rows 0..5, three pipes
   {
     const int m = 23;
     rhmc_rj_config c = config(11, 6, 0.4, 0.3, 0.3);
-    c.n_pipes = 2;
+    c.n_pipes = 3;
     const int W = 3 * c.N_max;
     std::vector<double> q0((size_t)m * W, 0.);
     std::vector<int32_t> K0(m);
@@ -239,7 +239,7 @@ int main(int argc, char** argv) {
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "reserved");
     c = config(2, 4, 0.5, 0.25, 0.25);
-    c.n_pipes = 3;
+    c.n_pipes = 5;
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "n_pipes");
     c = config(2, 4, 0.5, 0.25, 0.25);

@@ -147,12 +147,13 @@ def test_dead_ends_are_rejected_and_threads_do_not_matter(rj):
     kw = dict(f_pos=True, Niter=25, Nsteps=2, dt=0.05, N_max=6, P_move=[0.2, 0.4, 0.4])
     _, r1 = _native(rj, _gym(), starts, seeds, kw, n_threads=1)
     q4, r4 = _native(rj, _gym(), starts, seeds, kw, n_threads=7)
-    q2, r2 = _native(rj, _gym(), starts, seeds, kw, n_threads=5, n_pipes=2)   # two halves
-    for k in r1:
-        if k != "phase_s":                            # wall times
-            assert np.array_equal(r1[k], r4[k]), k
-            assert np.array_equal(r1[k], r2[k]), k
-    assert all(np.array_equal(a, b) for a, b in zip(q4, q2))
+    for pipes, t in ((2, 5), (3, 3), (4, 9)):        # that many parts on that many threads
+        qp, rp = _native(rj, _gym(), starts, seeds, kw, n_threads=t, n_pipes=pipes)
+        for k in r1:
+            if k != "phase_s":                        # wall times
+                assert np.array_equal(r1[k], r4[k]), k
+                assert np.array_equal(r1[k], rp[k]), (k, pipes)
+        assert all(np.array_equal(a, b) for a, b in zip(q4, qp))
     assert (r1["phase_s"] >= 0).all() and r1["phase_s"].sum() > 0
     fl = r1["flags"].astype(bool)
     assert fl.any()
@@ -233,7 +234,7 @@ def _inplace(g, q, p, ns):
     p[:] = pp
 
 
-@pytest.mark.parametrize("n_pipes", [1, 2])
+@pytest.mark.parametrize("n_pipes", [1, 2, 4])
 def test_checkpoint_resume_is_one_run(rj, n_pipes):
     """One run == a run, then a resume from its final q, K and states:
     bit-identical records (the checkpoint of the
