@@ -594,6 +594,15 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
   }
   const int64_t rows_n = (int64_t)cfg->n_iter + 1;
   std::vector<double> V0((size_t)n), V1((size_t)n), T0((size_t)n);
+  // V of every chain's q at the end of the previous iteration (V(q') if it
+  // accepted, else its V(q)) and the prior parameters it was computed with:
+  // while a schedule leaves them unchanged, an iteration's V(q) is that value
+  // (the engine's V of a chain does not depend on the batch it is in:
+  // tests/test_gpu_rj_native.py recomputes every recorded V), saving one
+  // engine phase per iteration
+  std::vector<double> V_end((size_t)n);
+  double V_end_g_ff2 = 0., V_end_beta = 0.;
+  bool V_end_ok = false;
   double phase[7] = {0, 0, 0, 0, 0, 0, 0};
   auto clk = std::chrono::steady_clock::now();
   auto lap = [&](int i) {  // the time since the last lap goes to phase i
@@ -626,21 +635,23 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
     });
     lap(0);
     // 2. V(q)
-    if (int rc = R.energies(all, V0)) return rc;
+    if (V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta) {
+      V0 = V_end;
+    } else if (int rc = R.energies(all, V0)) {
+      return rc;
+    }
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
       h.E0 = V0[c] + T0[c];
       const int64_t r = l * rec_stride + rec_off + c;
       if (rec) {
-        if (rec->q_chain) {
+        if (rec->q_chain) {  // the state, zero-padded to 3 N_max
           double* row = rec->q_chain + r * W;
-          std::fill(row, row + W, 0.);
-          std::copy(h.q.begin(), h.q.end(), row);
+          std::fill(std::copy(h.q.begin(), h.q.end(), row), row + W, 0.);
         }
         if (rec->p_chain) {
           double* row = rec->p_chain + r * W;
-          std::fill(row, row + W, 0.);
-          std::copy(h.p.begin(), h.p.end(), row);
+          std::fill(std::copy(h.p.begin(), h.p.end(), row), row + W, 0.);
         }
         if (rec->V_chain) rec->V_chain[r] = V0[c];
         if (rec->T_chain) rec->T_chain[r] = T0[c];
@@ -706,12 +717,16 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
           h.K = h.K0;
         }
       }
+      V_end[c] = acc ? V1[c] : V0[c];
       if (rec) {
         if (rec->accept) rec->accept[r] = acc ? 1 : 0;
         if (rec->flags) rec->flags[r] = h.dead ? (int32_t)RHMC_RJ_DEAD_END : 0;
       }
     });
     lap(6);
+    V_end_g_ff2 = R.P.g_ff2;
+    V_end_beta = R.P.beta;
+    V_end_ok = true;
   }
   if (phase_out)
     for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];

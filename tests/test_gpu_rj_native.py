@@ -137,6 +137,40 @@ def test_native_two_pipes_equal_one(gpu_lib):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
 
 
+@pytest.mark.parametrize("sched", [False, True])
+def test_native_recorded_V_is_the_engine_V_of_each_start(gpu_lib, sched):
+    """The driver takes an iteration's V(q) from the previous iteration's end
+    (V(q') when it accepted, its V(q) otherwise) while the prior parameters
+    are unchanged; the reference recomputes it.  Every recorded V_chain row
+    equals the engine's V of that row's q evaluated alone (one chain per
+    call), bit for bit: one- to five-star chains (the one-star register-window
+    energy and the per-wave kernels), with and without a g_ff2 schedule
+    (which forces the recomputation on the iterations it changes)."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+    g = _gym(par)
+    g.D = z[name + "/D"]
+    rs = np.random.RandomState(21)
+    starts = [m[:1 + c % 5] for c, m in enumerate(_starts(z[name + "/q_model"], 40, rs))]
+    kw = dict(f_pos=True, delta=1e-6, Niter=10, Nsteps=6, dt=0.05, N_max=8,
+              P_move=[0.4, 0.3, 0.3])
+    if sched:
+        kw["schedule_g_ff2"] = np.array([1., 1., 2., 2., 2., 4.])
+    g.run_RHMC_rj_batched([m.copy() for m in starts], list(range(300, 340)), **kw)
+    ctx = g._context()
+    gff = np.ravel(kw.get("schedule_g_ff2", [g.g_ff2]))
+    for l in range(kw["Niter"] + 1):
+        g.g_ff2 = float(gff[min(l, gff.size - 1)])
+        P = g._params(kw["delta"], 1000, for_energy=True)
+        for c in range(len(starts)):
+            K = int(g.N_chain[l, c])
+            V, _ = ctx.energy(P, g.q_chain[l, c, :3 * K], f_pos=True)
+            assert V == g.V_chain[l, c] or (np.isnan(V) and np.isnan(g.V_chain[l, c])), (l, c, K)
+    assert (g.A_chain & (g.move_chain > 0)).any()
+    assert set(np.unique(g.N_chain)) >= {1, 2, 3}
+
+
 def test_native_checkpoint_resume_on_the_engine(gpu_lib):
     """A run of Niter = 11 (rows 0..11) == a run of Niter = 5 and a resume from
     its final q and rj_rng_states for Niter = 5 more: the same engine batches
