@@ -74,7 +74,8 @@ double kinetic(const double* p, const double* H, int64_t d, std::vector<double>&
   tmp.resize((size_t)d);
   for (int64_t i = 0; i < d; ++i) tmp[i] = (p[i] * p[i]) / H[i];
   const double s1 = rhmc_np::pairwise_sum(tmp.data(), d);
-  for (int64_t i = 0; i < d; ++i) tmp[i] = std::log(std::fabs(H[i]));
+  for (int64_t i = 0; i < d; ++i)  // a star's two position entries share H: one log
+    tmp[i] = (i % 3 == 2 && H[i] == H[i - 1]) ? tmp[i - 1] : std::log(std::fabs(H[i]));
   const double s2 = rhmc_np::pairwise_sum(tmp.data(), d);
   return (s1 + s2) / 2.;
 }

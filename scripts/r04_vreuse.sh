@@ -3,7 +3,7 @@
 # recorded V recomputed alone, checkpoint, goldens), then throughput at
 # big-sim4 geometry and the bench --mode rj line.  Logs under gpurun_out/r04_vreuse/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-O=gpurun_out/r04_vreuse
+O=${OUT:-gpurun_out/r04_vreuse}
 mkdir -p $O
 export TMPDIR=/tmp
 step() {
