@@ -1001,10 +1001,12 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
     const int nt = host_threads(cfg);
     // pipe i takes streams i, i + pipes, ... (the HIP calls of the *_device
     // entry points touch no shared context state)
+    hipStream_t all_s[kStreams];
+    std::copy(E[0].s, E[0].s + kStreams, all_s);
     for (int i = 0; i < pipes; ++i) {
       E[i].dev = E[0].dev;
       E[i].ns = 0;
-      for (int j = i; j < kStreams; j += pipes) E[i].s[E[i].ns++] = E[0].s[j];
+      for (int j = i; j < kStreams; j += pipes) E[i].s[E[i].ns++] = all_s[j];
     }
     const int64_t W = 3 * (int64_t)cfg->N_max;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};

@@ -2,7 +2,7 @@
 # The checkpoint GPU tests, then native RJ throughput at big-sim4 geometry for
 # 1-4 pipes at 4,096 and 16,384 chains.  Logs under gpurun_out/r04_pipes/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
-O=gpurun_out/r04_pipes
+O=${OUT:-gpurun_out/r04_pipes}
 mkdir -p $O
 export TMPDIR=/tmp
 step() {
