@@ -956,9 +956,10 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
 }
 
 int pipes_for(const rhmc_rj_config* cfg, int64_t n) {
-  // default: measured at big-sim4 geometry (profiles/r04_pipes/): 2 pipes
-  // from 1,024 chains, 4 from 16,384 (1.39x one pipe there; 3 and 4 lose at 4,096)
-  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 16384 ? 4 : n >= 1024 ? 2 : 1);
+  // default: measured at big-sim4 geometry (profiles/r04_pipes2/): 2 pipes
+  // from 1,024 chains (1.11x one at 4,096; 3 and 4 lose there), 3 from 16,384
+  // (1.54x one, 1.16x two or four)
+  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 16384 ? 3 : n >= 1024 ? 2 : 1);
   return (int)std::max<int64_t>(1, std::min<int64_t>(pipes, n));
 }
 

@@ -86,7 +86,7 @@ typedef struct rhmc_rj_config {
                             of multi_gym.run_RHMC_rj_batched); 2..4: the chains in
                             that many contiguous parts on as many host threads, so
                             one part's host work overlaps the others' GPU work; 0:
-                            2 from 1,024 chains, 4 from 16,384                       */
+                            2 from 1,024 chains, 3 from 16,384                       */
   int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
                             seeds[c] (a checkpoint of an earlier run, or any
                             RandomState's get_state(): continue its stream)        */
