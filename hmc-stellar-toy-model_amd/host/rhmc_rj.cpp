@@ -622,7 +622,12 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
       h.H.resize((size_t)d);
       M.all(h.q.data(), d, h.H.data());
       h.p.resize((size_t)d);
-      for (int64_t i = 0; i < d; ++i) h.p[i] = h.rng.gauss() * std::sqrt(h.H[i]);
+      for (int64_t i = 0; i < d; i += 3) {  // p = randn(3K) * sqrt(H); H_y = H_x
+        const double sf = std::sqrt(h.H[i]), sx = std::sqrt(h.H[i + 1]);
+        h.p[i] = h.rng.gauss() * sf;
+        h.p[i + 1] = h.rng.gauss() * sx;
+        h.p[i + 2] = h.rng.gauss() * (h.H[i + 2] == h.H[i + 1] ? sx : std::sqrt(h.H[i + 2]));
+      }
       h.move = (int)choice(h.rng, cfg->P_move, 3, h.cdf);
       h.grow = false;
       if (h.move != 0) {
