@@ -279,3 +279,19 @@ def test_state_errors(rj):
         rj.run(P, q, None, **base, states=bad)
     with pytest.raises(ValueError, match="seed"):
         rj.run(P, q, None, **base)
+
+
+def test_integration_stub_matches_the_config_layout(rj):
+    """INTEGRATION.md's ctypes stub of rhmc_rj_config has the library's field
+    names, offsets and size (a maintainer copies it as it is)."""
+    import ctypes
+    import os
+    from conftest import ROOT
+    s = open(os.path.join(ROOT, "INTEGRATION.md")).read()
+    i = s.index("class _RjConfig")
+    ns = {"ctypes": ctypes}
+    exec(s[i:s.index("\n\n", i)], ns)
+    A, B = ns["_RjConfig"], rj.RjConfig
+    assert [f[0] for f in A._fields_] == [f[0] for f in B._fields_]
+    assert ctypes.sizeof(A) == ctypes.sizeof(B)
+    assert all(getattr(A, f[0]).offset == getattr(B, f[0]).offset for f in B._fields_)
