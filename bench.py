@@ -312,24 +312,41 @@ def bench_rj(args, wl, gpu, world, rank):
     import torch.distributed as dist
     from rhmc_amd import sampler, shard
     from rhmc_amd.photometry import mag2flux
-    g = sampler.multi_gym(dt=0.05, g_xx=float(wl.params["g_xx"]), g_ff=float(wl.params["g_ff"]),
-                          g_ff2=float(wl.params["g_ff2"]))
-    g.num_rows, g.num_cols = wl.D.shape
-    g.use_prior, g.alpha = True, 2.
-    g.fmin = mag2flux(23.3) * g.flux_to_count
-    g.fmax = mag2flux(15.) * g.flux_to_count
-    g.D = wl.D
-    g.device = gpu
-    starts = []
-    for c in range(wl.n_chains):
-        m = wl.q0[c].reshape(-1, 3).copy()
-        m[:, 0] = np.minimum(g.flux2mag_converter(m[:, 0]), 22.5)   # above the flux wall
-        starts.append(m)
-    leap = args.leap or 20
     n_it = args.mh_iter
-    kw = dict(Niter=n_it - 1, Nsteps=leap, dt=0.05, N_max=min(256, 2 * wl.K + 20),
-              P_move=[0.6, 0.2, 0.2])
-    seeds = [1000 * rank + c for c in range(wl.n_chains)]
+    if wl is None:
+        # BIGSIM4: the reference's flagship run as written (RHMC-big-sim4.py:
+        # 51 true stars on 32x32, every chain from its 5 model stars, K grows by
+        # births / splits, N_max 120, Nsteps 10, dt 0.05, beta_a = beta_b = 4)
+        from rhmc_amd import big_sim4
+        saved = np.random.get_state()
+        g, _, q_model = big_sim4.setup()
+        np.random.set_state(saved)
+        n_chains = args.chains or 4096
+        starts = [q_model.copy() for _ in range(n_chains)]
+        leap = args.leap or big_sim4.RUN_KW["Nsteps"]
+        kw = dict(Niter=n_it - 1, Nsteps=leap, dt=big_sim4.RUN_KW["dt"],
+                  N_max=big_sim4.RUN_KW["N_max"], P_move=big_sim4.RUN_KW["P_move"])
+        name, K0, D = "BIGSIM4", big_sim4.N_MODEL, g.D
+    else:
+        g = sampler.multi_gym(dt=0.05, g_xx=float(wl.params["g_xx"]),
+                              g_ff=float(wl.params["g_ff"]), g_ff2=float(wl.params["g_ff2"]))
+        g.num_rows, g.num_cols = wl.D.shape
+        g.use_prior, g.alpha = True, 2.
+        g.fmin = mag2flux(23.3) * g.flux_to_count
+        g.fmax = mag2flux(15.) * g.flux_to_count
+        g.D = wl.D
+        n_chains = wl.n_chains
+        starts = []
+        for c in range(n_chains):
+            m = wl.q0[c].reshape(-1, 3).copy()
+            m[:, 0] = np.minimum(g.flux2mag_converter(m[:, 0]), 22.5)   # above the flux wall
+            starts.append(m)
+        leap = args.leap or 20
+        kw = dict(Niter=n_it - 1, Nsteps=leap, dt=0.05, N_max=min(256, 2 * wl.K + 20),
+                  P_move=[0.6, 0.2, 0.2])
+        name, K0, D = wl.name, wl.K, wl.D
+    g.device = gpu
+    seeds = [1000 * rank + c for c in range(n_chains)]
     for _ in range(args.warmup):
         g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, **kw)
     if world > 1:
@@ -347,19 +364,21 @@ def bench_rj(args, wl, gpu, world, rank):
         steps = int(shard.sum_over_ranks(steps))
     res = {
         "metric": "chain-leapfrog-steps/sec, reversible-jump run_RHMC (%s %dx%d, K0=%d, "
-                  "%d chains/GPU)" % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K, wl.n_chains),
+                  "%d chains/GPU)" % (name, D.shape[0], D.shape[1], K0, n_chains),
         "value": steps / wall, "unit": "chain-leapfrog-steps/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": wall / args.steps * 1e3,
         "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": "synthetic (%s image and starts, chain seeds 1000 rank + c)" % wl.name,
+        "data": "synthetic (%s image and starts, chain seeds 1000 rank + c)" % name,
         "config": {"workload": "%s: %dx%d image, K0=%d, %d chains/GPU, %d iterations of %d "
-                               "steps per run, P_move [0.6, 0.2, 0.2], N_max %d"
-                               % (wl.name, wl.D.shape[0], wl.D.shape[1], wl.K, wl.n_chains,
-                                  n_it, leap, kw["N_max"]), "mode": "rj",
-                   "parallelism": "chain-sharded x%d" % world},
+                               "steps per run, P_move %s, N_max %d, beta_a = beta_b = %g"
+                               % (name, D.shape[0], D.shape[1], K0, n_chains, n_it, leap,
+                                  kw["P_move"], kw["N_max"], g.beta_a),
+                   "mode": "rj", "parallelism": "chain-sharded x%d" % world},
         "roofline": None,
         "rj": {"accept_rate_jumps": float(np.mean(g.A_chain[g.move_chain > 0]))
                if (g.move_chain > 0).any() else None,
+               "accept_rate_within": float(np.mean(g.A_chain[g.move_chain == 0]))
+               if (g.move_chain == 0).any() else None,
                "star_counts_end": [int(g.N_chain[-1].min()), int(g.N_chain[-1].max())],
                "dead_end_iterations": int(np.sum(g.flag_chain != 0)),
                "phase_ms_per_iteration": {k: v * 1e3 / n_it for k, v in g.rj_phase_s.items()},
@@ -434,6 +453,14 @@ def main():
     _fault_injection(rank)
 
     from rhmc_amd import shard, workloads
+    if args.workload.upper() == "BIGSIM4":
+        if args.mode != "rj":
+            raise SystemExit("bench.py: --workload BIGSIM4 is the reversible-jump flagship "
+                             "(--mode rj)")
+        if world > 1:
+            init_gloo(args.timeout)
+        return bench_rj(args, None, int(os.environ.get("RHMC_BENCH_DEVICE", local_rank)), world,
+                        rank)
     if args.workload.upper() in ("C4", "C5") and not args.chains and not args.global_chains:
         # C4 is one 2^20-chain set, C5 one 8192-chain set, sharded over the
         # ranks (BASELINE configs[3], [4]: "... across 8x MI355X")
@@ -485,14 +512,23 @@ def main():
 
     if args.mode == "datagen":
         return bench_datagen(args, wl, P, ctx, dev, stream, world, rank)
+    mh_acc = None
     if args.mode == "mh":
         leap = args.leap or 10
         if args.mh_unfused:
             ctx.set_option(capi.OPT_MH_FUSED, 0)
+        if args.f_pos:
+            # with f_pos a start below the flux wall has V = inf: every proposal
+            # would be rejected before any pixel work (workloads.mh_start)
+            q.copy_(torch.from_numpy(workloads.mh_start(wl)).to(dev))
+        # the accept decisions of each launch (n_iter x n_chains int32 on the device)
+        mh_acc = torch.zeros((args.mh_iter, wl.n_chains), dtype=torch.int32, device=dev)
+        mh_rec = capi.MhRecord(None, None, None, None, mh_acc.data_ptr())
 
         def launch():
             ctx.mh_device(P, q.data_ptr(), wl.n_chains, wl.K, args.mh_iter, leap,
-                          f_pos=bool(args.f_pos), seed=1234 + rank, stream=stream.cuda_stream)
+                          f_pos=bool(args.f_pos), seed=1234 + rank, record=mh_rec,
+                          stream=stream.cuda_stream)
     elif args.mode == "integrate":
         solver = {"hmc": capi.SOLVER_HMC, "naive": capi.SOLVER_RHMC_NAIVE,
                   "leap_frog": capi.SOLVER_RHMC_LEAPFROG}[args.solver]
@@ -597,6 +633,8 @@ def main():
         "roofline": roofline(pmc, wl, chain_steps, launch_ms, stale),
         "nonfinite_chains": nonfinite,
         "fixed_point_iters_per_step": fp_stats,
+        "mh_accept_rate_last_launch": (None if mh_acc is None
+                                       else float(mh_acc.float().mean().item())),
         "per_rank": per_rank,
         # the kernel sources this line ran (sha256/16 of csrc/*, Makefile, rhmc.h:
         # the same hash pmc_summary.py stores; the GPU box has no .git)
@@ -631,7 +669,7 @@ def roofline(pmc, wl, chain_steps, launch_ms, stale=False):
     if stale:
         pmc = dict(pmc, hbm_bytes_per_launch=None, fp64_flops_per_chain_step=None,
                    valu_active_frac=None, simd_valu_issue_frac=None,
-                   valu_insts_per_chain_step=None)
+                   valu_insts_per_chain_step=None, waves_per_simd_resident=None)
     traffic = pmc.get("hbm_bytes_per_launch")
     per = pmc.get("chain_steps_per_dispatch")
     if traffic is not None and per not in (None, chain_steps):
@@ -641,10 +679,17 @@ def roofline(pmc, wl, chain_steps, launch_ms, stale=False):
     bpu = alg_bytes_per_step(npix, wl.K)
     alg_gbs = bpu * chain_steps / s / 1e9
     achieved = None if fpc is None else fpc * chain_steps / s / 1e12
+    frac = None if achieved is None else achieved / FP64_PEAK_TFLOPS
+    ceil = issue_ceiling(pmc.get("waves_per_simd_resident"))
     return {
         "bound": "valu-fp64", "unit": "TFLOP/s", "peak": FP64_PEAK_TFLOPS,
         "achieved": achieved,
-        "frac": None if achieved is None else achieved / FP64_PEAK_TFLOPS,
+        "frac": frac,
+        # what the kernel's occupancy allows of that peak even on a stream of
+        # independent fp64 FMAs: `frac` is read against this (C2: one wave per SIMD)
+        "issue_ceiling": ceil,
+        "frac_of_issue_ceiling": (None if frac is None or ceil is None
+                                  else frac / ceil["value"]),
         "traffic": traffic,
         "kernel_ms": launch_ms,
         "chain_steps_per_launch": chain_steps,
@@ -667,6 +712,30 @@ def roofline(pmc, wl, chain_steps, launch_ms, stale=False):
                     "exceeds the HBM peak by construction: the image is read from "
                     "LDS/VGPRs, not HBM, so this is not a bound"},
     }
+
+
+# cycles per independent fp64 FMA wave-instruction on one SIMD at 1 / 2 / 4
+# resident waves (tools/isa_bench.hip on MI355X, DESIGN.md §4 Roofline); a
+# full-rate issue is 4 cycles per wave-instruction
+FMA_CYCLES_BY_WAVES = ((1.0, 9.6), (2.0, 6.4), (4.0, 5.5))
+
+
+def issue_ceiling(waves):
+    """The fraction of the fp64 peak that `waves` resident waves per SIMD can
+    issue on a stream of independent FMAs: 4 / cycles per wave-instruction,
+    interpolated linearly in the measured table (clamped at its ends)."""
+    if waves is None:
+        return None
+    pts = FMA_CYCLES_BY_WAVES
+    w = min(max(float(waves), pts[0][0]), pts[-1][0])
+    for (w0, c0), (w1, c1) in zip(pts, pts[1:]):
+        if w <= w1:
+            cyc = c0 + (c1 - c0) * (w - w0) / (w1 - w0)
+            break
+    return {"value": 4.0 / cyc, "waves_per_simd": float(waves),
+            "note": "4 cycles / measured cycles per independent fp64 FMA wave-instruction "
+                    "at this many resident waves per SIMD (9.6 / 6.4 / 5.5 cycles at "
+                    "1 / 2 / 4 waves, tools/isa_bench.hip)"}
 
 
 def init_gloo(timeout):

@@ -1082,24 +1082,32 @@ bool use_windowed(const rhmc_ctx* ctx, int K) {
   return need > (size_t)ctx->max_lds || force_windowed(ctx);
 }
 
-// Windowed kernels: W waves per workgroup, LDS = W * tables.
-void pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
+// Windowed kernels: W waves per workgroup, LDS = W * tables (K <= 256: 136 KB
+// for one wave, within gfx950's 160 KB; a device with less LDS gets
+// RHMC_ERR_UNSUPPORTED here, not a failed launch).
+int pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
   int w = 4;
   while (w > 1 && WinG::lds_bytes(w, K) > (size_t)ctx->max_lds) w >>= 1;
   *W = w;
-  *lds = WinG::lds_bytes(w, K);  // K <= 256: 136 KB for one wave, within the CU's 160 KB
+  *lds = WinG::lds_bytes(w, K);
+  if (*lds > (size_t)ctx->max_lds)
+    return fail(RHMC_ERR_UNSUPPORTED, "windowed PSF tables for K = " + std::to_string(K) +
+                                          " exceed the device's LDS (" + std::to_string(*lds) +
+                                          " B > " + std::to_string(ctx->max_lds) + " B)");
+  return RHMC_OK;
 }
 
 // The slotted kernels' workgroup for a path (with_path): the windowed tables'
 // LDS as above, or four waves of the dense kernel (32 px: 41.5 KB, 48 px:
 // 92.6 KB).
-void pick_waves_path(const rhmc_ctx* ctx, int path, int K, size_t* lds, int* W) {
+int pick_waves_path(const rhmc_ctx* ctx, int path, int K, size_t* lds, int* W) {
   if (path == 32 || path == 48) {
     *W = 4;
     *lds = path == 32 ? DenseG<32>::lds_bytes(4) : DenseG<48>::lds_bytes(4);
-    return;
+    if (*lds > (size_t)ctx->max_lds) return fail(RHMC_ERR_UNSUPPORTED, "dense kernel LDS");
+    return RHMC_OK;
   }
-  pick_waves_win(ctx, K, lds, W);
+  return pick_waves_win(ctx, K, lds, W);
 }
 
 // The dense many-star kernel (rhmc_dense.hpp) for (K, image): by default from
@@ -1406,8 +1414,10 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
     W = 4;
     while (W > 1 && WinEG::lds_bytes(W, K) > (size_t)ctx->max_lds) W >>= 1;
     lds = WinEG::lds_bytes(W, K);
+    if (lds > (size_t)ctx->max_lds)
+      return fail(RHMC_ERR_UNSUPPORTED, "windowed energy tables exceed the device's LDS");
   } else if (win) {
-    pick_waves_path(ctx, path, K, &lds, &W);
+    if ((rc = pick_waves_path(ctx, path, K, &lds, &W))) return rc;
   } else if ((rc = pick_waves(ctx, K, &lds, &W))) {
     return rc;
   }
@@ -1625,7 +1635,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.n_chains = n_chains;
     a.K = K;
     a.n_steps = n_steps;
-    pick_waves_path(ctx, path, K, &lds, &W);
+    if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
     return with_path(path, K, [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
@@ -2009,7 +2019,7 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
-  pick_waves_path(ctx, path, K, &lds, &W);
+  if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
@@ -2112,7 +2122,7 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   a.g = make_geometry(ctx->rows, ctx->cols);
   size_t lds;
   int W;
-  pick_waves_path(ctx, path, K, &lds, &W);
+  if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K, [&](auto gt, auto st) {
@@ -2376,10 +2386,11 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   const int path = dense_path(ctx, K, a.c);
   const bool win = path || use_windowed(ctx, K);
   if (win && !path && !window_exact(a.c)) return window_unsupported();
-  if (win)
-    pick_waves_path(ctx, path, K, &lds, &W);
-  else if ((rc = pick_waves(ctx, K, &lds, &W)))
+  if (win) {
+    if ((rc = pick_waves_path(ctx, path, K, &lds, &W))) return rc;
+  } else if ((rc = pick_waves(ctx, K, &lds, &W))) {
     return rc;
+  }
   const size_t sb = (size_t)n_chains * 3 * K * sizeof(double);
   HIP_TRY(hipSetDevice(ctx->device));
   if ((rc = ensure_scratch(ctx, 2 * sb + 256))) return rc;

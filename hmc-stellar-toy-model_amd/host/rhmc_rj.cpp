@@ -27,6 +27,7 @@
 #include <functional>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <mutex>
 #include <string>
@@ -130,18 +131,17 @@ struct BetaDist {
 class Pool {
  public:
   explicit Pool(int n) {
-    for (int t = 1; t < n; ++t) th_.emplace_back([this] { worker(); });
-  }
-  ~Pool() {
-    {
-      std::lock_guard<std::mutex> l(mu_);
-      stop_ = true;
+    try {
+      for (int t = 1; t < n; ++t) th_.emplace_back([this] { worker(); });
+    } catch (...) {  // a thread could not start: stop and join the ones that did
+      shutdown();
+      throw;
     }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
   }
+  ~Pool() { shutdown(); }
   int size() const { return (int)th_.size() + 1; }
-  // body(i) for i in [0, n), chunks of 16, the caller works too
+  // body(i) for i in [0, n), chunks of 16, the caller works too.  An exception
+  // from body (any thread) is rethrown here once every thread has left it.
   void run(int64_t n, const std::function<void(int64_t)>& body) {
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -149,6 +149,7 @@ class Pool {
       n_ = n;
       next_.store(0);
       busy_ = (int)th_.size();
+      exc_ = nullptr;
       ++gen_;
     }
     cv_.notify_all();
@@ -156,15 +157,35 @@ class Pool {
     std::unique_lock<std::mutex> l(mu_);
     done_.wait(l, [this] { return busy_ == 0; });
     body_ = nullptr;
+    if (exc_) {
+      std::exception_ptr e = exc_;
+      exc_ = nullptr;
+      std::rethrow_exception(e);
+    }
   }
 
  private:
+  void shutdown() {
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+    th_.clear();
+  }
   void work() {
-    for (;;) {
-      const int64_t b = next_.fetch_add(16);
-      if (b >= n_) return;
-      const int64_t e = std::min(n_, b + 16);
-      for (int64_t i = b; i < e; ++i) (*body_)(i);
+    try {
+      for (;;) {
+        const int64_t b = next_.fetch_add(16);
+        if (b >= n_) return;
+        const int64_t e = std::min(n_, b + 16);
+        for (int64_t i = b; i < e; ++i) (*body_)(i);
+      }
+    } catch (...) {  // keep the first; the other chunks still drain
+      std::lock_guard<std::mutex> l(mu_);
+      if (!exc_) exc_ = std::current_exception();
+      next_.store(n_);
     }
   }
   void worker() {
@@ -190,6 +211,7 @@ class Pool {
   int busy_ = 0;
   uint64_t gen_ = 0;
   bool stop_ = false;
+  std::exception_ptr exc_;
 };
 
 // ------------------------------------------------------------------- chains
@@ -931,7 +953,26 @@ int ctx_energy_staged(void* user, const rhmc_params* P, int32_t G, const int32_t
 // failing part's error is the one reported.
 template <class Body>
 int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
-  if (pipes <= 1) return body(0, 0, n, nt, phase);
+  // one part's body on this thread; an exception becomes an error code (no
+  // C++ exception may cross the ABI, and none may leave a std::thread)
+  auto guarded = [&](int i, int64_t f, int64_t m, int t, double* ph, std::string& err) {
+    try {
+      const int rc = body(i, f, m, t, ph);
+      if (rc) err = g_err;
+      return rc;
+    } catch (const std::exception& e) {
+      err = std::string("host exception: ") + e.what();
+    } catch (...) {
+      err = "host exception";
+    }
+    return (int)RHMC_ERR_NOMEM;
+  };
+  if (pipes <= 1) {
+    std::string err;
+    const int rc = guarded(0, 0, n, nt, phase, err);
+    if (rc) g_err = err;
+    return rc;
+  }
   std::vector<int64_t> first((size_t)pipes + 1);
   for (int i = 0; i <= pipes; ++i) first[i] = n * i / pipes;
   std::vector<int> threads((size_t)pipes);
@@ -940,15 +981,20 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
   std::vector<int> rcs((size_t)pipes, 0);
   std::vector<std::string> errs((size_t)pipes);
   std::vector<std::thread> ts;
-  for (int i = 1; i < pipes; ++i)
-    ts.emplace_back([&, i] {
-      ph[i].fill(0.);
-      rcs[i] = body(i, first[i], first[i + 1] - first[i], threads[i], ph[i].data());
-      if (rcs[i]) errs[i] = g_err;
-    });
+  ts.reserve((size_t)pipes);
+  for (int i = 1; i < pipes; ++i) {
+    ph[i].fill(0.);
+    try {
+      ts.emplace_back([&, i] {
+        rcs[i] = guarded(i, first[i], first[i + 1] - first[i], threads[i], ph[i].data(), errs[i]);
+      });
+    } catch (const std::exception& e) {  // this part does not run: report it
+      rcs[i] = RHMC_ERR_NOMEM;
+      errs[i] = std::string("cannot start a pipe thread: ") + e.what();
+    }
+  }
   ph[0].fill(0.);
-  rcs[0] = body(0, first[0], first[1] - first[0], threads[0], ph[0].data());
-  if (rcs[0]) errs[0] = g_err;
+  rcs[0] = guarded(0, first[0], first[1] - first[0], threads[0], ph[0].data(), errs[0]);
   for (auto& t : ts) t.join();
   for (int i = 0; i < pipes; ++i)
     for (int k = 0; k < 7; ++k) phase[k] += ph[i][k];
@@ -1051,6 +1097,18 @@ int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, do
       case 5: out[i] = r.standard_exponential(); break;
       default: return fail(RHMC_ERR_ARG, "unknown kind");
     }
+  }
+  return 0;
+}
+
+int rhmc_rj_beta_eval(double a, double b, const double* x, int64_t n, double* pdf, double* logpdf) {
+  if (!(a > 0) || !(b > 0)) return fail(RHMC_ERR_ARG, "beta_a and beta_b must be > 0");
+  if (n < 0 || (n > 0 && !x)) return fail(RHMC_ERR_ARG, "bad n or x");
+  BetaDist d;
+  d.set(a, b);
+  for (int64_t i = 0; i < n; ++i) {
+    if (pdf) pdf[i] = d.pdf(x[i]);
+    if (logpdf) logpdf[i] = d.logpdf(x[i]);
   }
   return 0;
 }

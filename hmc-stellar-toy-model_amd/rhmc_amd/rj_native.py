@@ -16,7 +16,8 @@ from . import capi
 LIB_PATH = os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so")
 DEAD_END = 1                 # RHMC_RJ_DEAD_END
 
-EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_last_error")
+EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_beta_eval",
+           "rhmc_rj_last_error")
 
 ENERGY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
                              ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int32,
@@ -89,6 +90,7 @@ def _load():
                                 ctypes.c_int64, P(RjRecord)],
         "rhmc_np_draws": [ctypes.c_uint32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                           ctypes.c_int64, vp],
+        "rhmc_rj_beta_eval": [ctypes.c_double, ctypes.c_double, vp, ctypes.c_int64, vp, vp],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -121,6 +123,16 @@ def np_draws(seed, kind, n, a=0., b=0.):
     _check(_lib.rhmc_np_draws(int(seed), kinds[kind], float(a), float(b), int(n),
                               out.ctypes.data))
     return out
+
+
+def beta_eval(a, b, x):
+    """The moves' Beta(a, b) pdf and logpdf as the driver evaluates them
+    (scipy.stats.beta at sampler_RHMC.py:1342, :1363, :1438) -> (pdf, logpdf)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    pdf, logpdf = np.empty_like(x), np.empty_like(x)
+    _check(_lib.rhmc_rj_beta_eval(float(a), float(b), x.ctypes.data, x.size, pdf.ctypes.data,
+                                  logpdf.ctypes.data))
+    return pdf, logpdf
 
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,

@@ -713,6 +713,11 @@ class multi_gym(base_class):
         one uninterrupted run); engine="python" is the NumPy loop below (the
         reference's own draws through np.random)."""
         n = len(q_models_0)
+        # any array-like schedule, on either engine (the NumPy loop reads .size)
+        if schedule_g_ff2 is not None:
+            schedule_g_ff2 = np.ravel(np.asarray(schedule_g_ff2, dtype=np.float64))
+        if schedule_beta is not None:
+            schedule_beta = np.ravel(np.asarray(schedule_beta, dtype=np.float64))
         if engine == "native":
             if rng_states is None and (seeds is None or len(seeds) != n):
                 raise ValueError("one seed per chain")

@@ -15,6 +15,13 @@ Beyond BASELINE's configs, the reference's own many-star drivers (dense
 
 Randomness: numpy legacy RandomState; the image uses seed 77
 (RHMC-big-sim4.py:18), chain initial states seed 1000 (+ shard offset).
+
+MH starts (`mh_start`): the multi-star workloads draw magnitudes down to
+23.3, below the flux wall at mag 23 (f_lim, sampler_RHMC.py:194-196), so with
+run_RHMC's f_pos=True every such start has V = inf (sampler_RHMC.py:303-309)
+and every proposal is rejected before any pixel work.  For MH the chains
+start with every flux raised to at least 1.5 f_lim (mag 22.56); the leapfrog
+benches keep the plain starts (the flux wall reflections are part of C3/C5).
 """
 import re
 
@@ -65,6 +72,14 @@ def _powlaw_stars(rng, K, n, ftc, mag_lo=15., mag_hi=23.3, alpha=2.):
     x = rng.random_sample(K) * (n - 2.) + 1.
     y = rng.random_sample(K) * (n - 2.) + 1.
     return f, x, y
+
+
+def mh_start(wl, floor=1.5):
+    """The workload's chain starts for run_RHMC's MH loop with f_pos=True:
+    fluxes raised to >= floor * f_lim (positions and momenta unchanged)."""
+    q = wl.q0.copy()
+    q[:, 0::3] = np.maximum(q[:, 0::3], floor * wl.params["f_lim"])
+    return q
 
 
 def make(name, n_chains=None, seed_offset=0):

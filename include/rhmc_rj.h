@@ -145,6 +145,14 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
  * 5: standard_exponential(). */
 int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, double* out);
 
+/* The split / merge moves' Beta(beta_a, beta_b) density as the driver
+ * evaluates it (scipy.stats.beta.logpdf / pdf at sampler_RHMC.py:1342, :1363,
+ * :1438), for parity checks: n points x -> pdf[n], logpdf[n] (each nullable).
+ * Integer exponents a - 1, b - 1 <= 8 (the reference's defaults 2, 2 and
+ * RHMC-big-sim4.py's 4, 4) take the product form. */
+int rhmc_rj_beta_eval(double a, double b, const double* x, int64_t n, double* pdf,
+                      double* logpdf);
+
 const char* rhmc_rj_last_error(void);
 
 #ifdef __cplusplus

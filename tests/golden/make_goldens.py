@@ -683,6 +683,170 @@ def case_rj(S, U):
     return out
 
 
+def _jitter_model(stars, rs, dmag=0.05, dpos=0.2):
+    m = np.array(stars, dtype=float).copy()
+    m[:, 0] += dmag * rs.randn(len(m))
+    m[:, 1:] += dpos * rs.randn(len(m), 2)
+    return m
+
+
+def case_mh_bigk(S, U):
+    """multi_gym.run_RHMC move-0 (P_move = [1, 0, 0], f_pos = True,
+    sampler_RHMC.py:1018-1083) at many stars, every start above the flux wall
+    (V finite, sampler_RHMC.py:303-309), so that proposals are really accepted
+    and rejected — the generator requires 0 < acceptance < 1 and tries seeds
+    until a run has both (the seed used is recorded).
+
+    d51: RHMC-big-sim4.py's geometry and parameters (32x32, 51 true stars from
+         its power law, mags 15-20, g_xx 0.05, g_ff = g_ff2 = 4, prior on,
+         RHMC-big-sim4.py:5-47), the model the truth jittered;
+    w64: the C5 geometry (256x256, K = 64, big-sim4 parameters, prior), mags
+         in [15, 22] (all above the wall at mag 23)."""
+    out = {}
+    for name, n, K, mags, niter, nsteps, seeds in [
+        ("d51", 32, 51, (20., 15.), 10, 5, range(500, 540)),
+        ("w64", 256, 64, (22., 15.), 8, 5, range(600, 640)),
+    ]:
+        np.random.seed(77)
+        g = make_gym(S, n=n, g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True,
+                     fminmax=mags)
+        stars = powlaw_stars(U, g, K, n, mag_lo=mags[1], mag_hi=mags[0])
+        g.gen_mock_data(stars)
+        model = _jitter_model(stars, np.random.RandomState(K))
+        assert (g.format_q(model.copy())[0::3] > 1.5 * g.f_lim).all()
+        for seed in seeds:
+            np.random.seed(seed)
+            with contextlib.redirect_stdout(io.StringIO()):
+                g.run_RHMC(model.copy(), f_pos=True, delta=1e-6, Niter=niter,
+                           Nsteps=nsteps, dt=0.05, N_max=K)
+            rate = g.A_chain.mean()
+            if 0 < rate < 1:
+                break
+        else:
+            raise RuntimeError("no seed with 0 < acceptance < 1 for " + name)
+        assert np.isfinite(g.E_chain).all()
+        res = dict(D=g.D, q_model=model, q_chain=g.q_chain, p_chain=g.p_chain,
+                   E_chain=g.E_chain, V_chain=g.V_chain, T_chain=g.T_chain,
+                   A_chain=g.A_chain.astype(np.int32), niter=niter, nsteps=nsteps,
+                   seed=seed, dt=0.05)
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+        print(name, "seed", seed, "accepted", g.A_chain.sum(), "of", niter + 1)
+    return out
+
+
+def case_rj_big(S, U):
+    """run_RHMC with the reversible-jump moves across K = 64 (the register-slot
+    boundary of the engine's one-wave-per-chain kernels): a 32x32 image of 100
+    true stars from RHMC-big-sim4.py's power law (alpha 2, mags 15-20), 64
+    model stars (the first 64 true stars, jittered; every flux above the wall,
+    so V is finite), RHMC-big-sim4.py's move parameters (P_move
+    [0.6, 0.2, 0.2], K_split 1, beta_a = beta_b = 4, N_max 120, prior on;
+    :10, :42-47, :77), 2 steps per trajectory.  The generator requires the
+    chain to grow past 65 stars and 0 < acceptance < 1."""
+    np.random.seed(77)
+    g = make_gym(S, n=32, g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True)
+    g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
+    stars = powlaw_stars(U, g, 100, 32, mag_lo=15., mag_hi=20.)
+    g.gen_mock_data(stars)
+    model = _jitter_model(stars[:64], np.random.RandomState(64))
+    assert (g.format_q(model.copy())[0::3] > 1.5 * g.f_lim).all()
+    niter, nsteps, P_move = 30, 2, [0.6, 0.2, 0.2]
+    for seed in range(800, 900):
+        np.random.seed(seed)
+        try:
+            with contextlib.redirect_stdout(io.StringIO()), np.errstate(all="ignore"):
+                g.run_RHMC(model.copy(), f_pos=True, delta=1e-6, Niter=niter, Nsteps=nsteps,
+                           dt=0.05, N_max=120, P_move=P_move)
+        except Exception:
+            continue
+        if g.N_chain.max() > 65 and 0 < g.A_chain.mean() < 1:
+            break
+    else:
+        raise RuntimeError("no seed grows past 64 stars")
+    res = dict(D=g.D, q_model=model, q_chain=g.q_chain, p_chain=g.p_chain,
+               E_chain=g.E_chain, V_chain=g.V_chain, T_chain=g.T_chain,
+               A_chain=g.A_chain.astype(np.int32), move_chain=g.move_chain,
+               N_chain=g.N_chain, P_move=np.array(P_move), niter=niter, nsteps=nsteps,
+               seed=seed, dt=0.05, N_max=120, K_split=1., beta_a=4., beta_b=4.)
+    out = pack("b64/", res)
+    out.update(pack("b64/par_", gym_params(g)))
+    print("rj_big seed", seed, "moves", np.bincount(g.move_chain, minlength=5),
+          "accepted", np.bincount(g.move_chain[g.A_chain], minlength=5),
+          "N", g.N_chain.min(), g.N_chain.max())
+    return {"rj_big": out}
+
+
+def case_flagship(S, U):
+    """The reference's flagship run, RHMC-big-sim4.py, as written except
+    Niter (40 instead of 10000) and verbose (off: it only prints and plots,
+    which draws nothing from the RNG): seed 77, 32x32, 51 true stars from the
+    power law (alpha 2, mags 15-20), 5 model stars, gen_mock_data,
+    gen_noise_profile(N_trial = 1000) (with the normed -> density shim), then
+    run_RHMC(f_pos, delta 1e-6, Nsteps 10, dt 0.05, P_move [0.6, 0.2, 0.2],
+    N_max 120) with K_split 1, beta_a = beta_b = 4, prior on
+    (RHMC-big-sim4.py:5-21, :39-47, :60-77).
+
+    Recorded: the data image, the truth and model stars, NumPy's global
+    stream state right before run_RHMC (so that a GPU test starts from it
+    without re-running the 1000 noise realisations) and right after
+    gen_mock_data, the noise histogram, and every chain record."""
+    g = S.multi_gym(dt=0., Nsteps=0, g_xx=0.05, g_ff=4., g_ff2=4.)
+    np.random.seed(77)
+    g.num_rows = g.num_cols = 32
+    n_true, n_model = int(32 ** 2 * 0.05), 5
+    alpha, mag_max, mag_min = 2., 20., 15.
+    fmin, fmax = g.mag2flux_converter(mag_max), g.mag2flux_converter(mag_min)
+    mag = g.flux2mag_converter(U.gen_pow_law_sample(alpha, fmin, fmax, n_true))
+    q_true = np.zeros((n_true, 3))
+    for i in range(n_true):
+        x = np.random.random() * (g.num_rows - 2.) + 1.
+        y = np.random.random() * (g.num_cols - 2.) + 1.
+        q_true[i] = np.array([mag[i], x, y])
+    g.fmin, g.fmax = fmin, fmax
+    g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
+    g.use_prior, g.alpha = True, alpha
+    q_model = np.zeros((n_model, 3))
+    q_model[:, 0] = g.flux2mag_converter(U.gen_pow_law_sample(alpha, fmin, fmax, n_model))
+    q_model[:, 1] = np.random.random(size=n_model) * (g.num_rows - 2.) + 1.
+    q_model[:, 2] = np.random.random(size=n_model) * (g.num_cols - 2.) + 1.
+    g.gen_mock_data(q_true)
+    st_data = np.random.get_state()
+    orig_hist = np.histogram
+
+    def hist_shim(a, bins=10, range=None, normed=None, weights=None, density=None):
+        return orig_hist(a, bins=bins, range=range, weights=weights,
+                         density=bool(normed) or bool(density))
+    np.histogram = hist_shim
+    try:
+        g.gen_noise_profile(q_true, N_trial=1000)
+    finally:
+        np.histogram = orig_hist
+    st_run = np.random.get_state()
+    niter, nsteps, dt, N_max, P_move = 40, 10, 5e-2, 120, [0.6, 0.2, 0.2]
+    with contextlib.redirect_stdout(io.StringIO()):
+        g.run_RHMC(q_model.copy(), f_pos=True, delta=1e-6, Niter=niter, Nsteps=nsteps,
+                   dt=dt, save_traj=False, verbose=False, q_true=q_true,
+                   schedule_beta=None, P_move=P_move, N_max=N_max)
+    res = dict(D=g.D, q_true=q_true, q_model=q_model,
+               rng_data_key=st_data[1], rng_data_pos=st_data[2],
+               rng_data_gauss=np.array([st_data[3], st_data[4]]),
+               rng_key=st_run[1], rng_pos=st_run[2],
+               rng_gauss=np.array([st_run[3], st_run[4]]),
+               hist_noise=g.hist_noise, centers_noise=g.centers_noise,
+               q_chain=g.q_chain, p_chain=g.p_chain, E_chain=g.E_chain,
+               V_chain=g.V_chain, T_chain=g.T_chain, A_chain=g.A_chain.astype(np.int32),
+               move_chain=g.move_chain, N_chain=g.N_chain, P_move=np.array(P_move),
+               niter=niter, nsteps=nsteps, dt=dt, N_max=N_max,
+               K_split=g.K_split, beta_a=g.beta_a, beta_b=g.beta_b)
+    out = pack("", res)
+    out.update(pack("par_", gym_params(g)))
+    print("flagship moves", np.bincount(g.move_chain, minlength=5),
+          "accepted", np.bincount(g.move_chain[g.A_chain], minlength=5),
+          "N", g.N_chain.min(), g.N_chain.max())
+    return {"flagship": out}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -708,9 +872,13 @@ def main():
             for name, d in case_trajs(S, U).items():
                 np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
                 print("wrote", name)
+        if not args.only or args.only == "mh_bigk":
+            np.savez_compressed(os.path.join(HERE, "mh_bigk.npz"), **case_mh_bigk(S, U))
+            print("wrote mh_bigk")
         # subsets of the above, regenerated on their own (--only c5 / bigk)
-        for job, fn in (("c5", case_c5), ("bigk", case_bigk)):
-            if args.only == job or (not args.only and job == "bigk"):
+        for job, fn in (("c5", case_c5), ("bigk", case_bigk), ("flagship", case_flagship),
+                        ("rj_big", case_rj_big)):
+            if args.only == job or (not args.only and job in ("bigk", "flagship", "rj_big")):
                 for name, d in fn(S, U).items():
                     np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
                     print("wrote", name)

@@ -34,6 +34,9 @@ def test_bench_json_line():
         assert r["frac"] is None and r["achieved"] is None
     else:
         assert r["frac"] == pytest.approx(r["achieved"] / r["peak"])
+        # C2 runs one wave per SIMD: the FMA issue ceiling there is 4 / 9.6
+        assert r["issue_ceiling"]["value"] == pytest.approx(4 / 9.6, rel=0.01)
+        assert r["frac_of_issue_ceiling"] == pytest.approx(r["frac"] / r["issue_ceiling"]["value"])
     # value counts wall time around the launches, kernel_ms the launches alone
     assert d["ms_per_step"] >= 0.9 * r["kernel_ms"]
     assert d["nonfinite_chains"] == 0

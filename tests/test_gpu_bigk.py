@@ -203,25 +203,53 @@ def _oracle_mh(m, q, z, u, n_iter, n_steps, f_pos=True):
     return np.array(acc), q
 
 
+def _bigk_mh_case(par, K=100, n=32, seed=31):
+    """A 32x32 image of K true stars (RHMC-big-sim4.py's power law, mags
+    15-20: every flux above the wall) and two chains at the truth, jittered
+    (flux x lognormal 2 %, 0.05 px): with f_pos=True V is finite, so the MH
+    test below really accepts and rejects."""
+    rs = np.random.RandomState(seed)
+    ftc = par["flux_to_count"]
+    fmin, fmax = R.mag2flux(20.) * ftc, R.mag2flux(15.) * ftc
+    u = rs.random_sample(K)                       # gen_pow_law_sample, alpha 2 (utils.py:460-471)
+    f = np.exp(np.log(fmin ** -1. + u * (fmax ** -1. - fmin ** -1.)) / -1.)
+    x = rs.random_sample(K) * (n - 2.) + 1.
+    y = rs.random_sample(K) * (n - 2.) + 1.
+    D = rs.poisson(R.model_image(n, n, np.stack([f, x, y], 1), par["B_count"],
+                                 par["fwhm_pix"])).astype(float)
+    q = np.empty((2, 3 * K))
+    q[:, 0::3] = f * np.exp(0.02 * rs.randn(2, K))
+    q[:, 1::3] = x + 0.05 * rs.randn(2, K)
+    q[:, 2::3] = y + 0.05 * rs.randn(2, K)
+    assert (q[:, 0::3] > 1.5 * par["f_lim"]).all()
+    return D, q
+
+
 def test_bigk_mh_vs_oracle(gpu_lib, bigk_kernel):
     """rhmc_mh (the four-kernel MH loop) at K = 100 with host draws: the
-    accept sequence and chains of the oracle's run_RHMC move-0 iterations."""
+    accept sequence and chains of the oracle's run_RHMC move-0 iterations.
+    The chains start above the flux wall (V finite), and the draws make both
+    chains accept and reject (checked: a reject-everything or
+    accept-everything MH fails)."""
     capi = gpu_lib
     z = load_golden("traj_bigk")
-    par = R.params_from_npz(z)
-    ctx = capi.Context(z["D"])
+    par = dict(R.params_from_npz(z), dt=0.1)
+    D, q0 = _bigk_mh_case(par)
+    ctx = capi.Context(D)
     P = capi_params(capi, par)           # V_prior_const for V's prior (:320-321)
-    m = R.RefModel(z["D"], par)
-    q0, _ = _bigk_batch(z, 2, 9)
-    n_iter, n_steps = 4, 3
-    rs = np.random.RandomState(10)
+    m = R.RefModel(D, par)
+    n_iter, n_steps = 6, 4
+    rs = np.random.RandomState(12)
     zz = rs.randn(n_iter, 2, q0.shape[1])
     uu = rs.rand(n_iter, 2)
     out = ctx.mh(P, q0, n_iter, n_steps, f_pos=True, z=zz, u=uu, record=True)
+    acc_all = out["accept"].astype(bool)
     for c in range(2):
         acc, qo = _oracle_mh(m, q0[c], zz[:, c], uu[:, c], n_iter, n_steps)
-        np.testing.assert_array_equal(out["accept"][:, c].astype(bool), acc)
+        assert 0 < acc.mean() < 1, acc
+        np.testing.assert_array_equal(acc_all[:, c], acc)
         assert_state_close(out["q"][c], qo, 1e-9, "mh q chain %d" % c)
+    assert np.isfinite(out["E_chain"]).all()
     ctx.close()
 
 
@@ -256,11 +284,14 @@ def test_k256_limit(gpu_lib, bigk_kernel):
     ctx.close()
 
 
-def test_run_RHMC_births_past_64(gpu_lib):
-    """RHMC-big-sim4.py-style transdimensional runs cross K = 64: births from
-    64 stars (birth_death_move, sampler_RHMC.py:1200-1240) followed by RHMC
-    steps, V and T at the new dimension agree with the oracle; and run_RHMC
-    with P_move = [0.6, 0.2, 0.2], N_max = 120 completes from 63 stars."""
+def test_births_past_64_then_steps(gpu_lib):
+    """Births from 64 stars (birth_death_move, sampler_RHMC.py:1200-1240; the
+    engine's one-wave-per-chain kernels change register slot count at 64)
+    followed by RHMC steps, V and T at the new dimension agree with the
+    oracle, every flux above the wall so that V(f_pos=True) is finite (a
+    32x32 image of 100 true stars, the chain at 64 of them).  The
+    reference's own run_RHMC across K = 64 (rj_big.npz) is
+    test_gpu_reference_runs.py::test_rj_big_run_RHMC_births_past_64."""
     from rhmc_amd.sampler import multi_gym
     zb = load_golden("traj_bigk")
     par = R.params_from_npz(zb)
@@ -270,29 +301,21 @@ def test_run_RHMC_births_past_64(gpu_lib):
     g.use_prior, g.alpha = True, 2.
     g.fmin, g.fmax = g.mag2flux_converter(20.), g.mag2flux_converter(15.)
     g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
-    g.D = zb["D"]
-    q = zb["Q"][0, 0][:3 * 64].copy()
-    p = zb["P"][0, 0][:3 * 64].copy()
+    D, qq = _bigk_mh_case(par)      # 100 true stars above the wall, chains near the truth
+    g.D = D
+    q = qq[0, :3 * 64].copy()       # 64 of them
+    p = np.random.RandomState(4).randn(3 * 64) * np.sqrt(g.H(q))
     g.Nobjs, g.d = 64, 192
     g.V(q, f_pos=True)        # caches V_prior_const (:320-321), as run_RHMC's first V does
     np.random.seed(5)
     for _ in range(3):                                    # 64 -> 67 stars
         q, p, _ = g.birth_death_move(q, p, True)
     assert g.Nobjs == 67 and q.size == 201
-    m = R.RefModel(zb["D"], dict(par, fmin=g.fmin, fmax=g.fmax))
-    q1, p1 = g.RHMC_steps(q, p, 3)
-    qo, po, _, _ = m.trajectory(q, p, 3, record=False)
+    m = R.RefModel(D, dict(par, fmin=g.fmin, fmax=g.fmax))
+    q1, p1 = g.RHMC_steps(q, p, 2)
+    qo, po, _, _ = m.trajectory(q, p, 2, record=False)
     assert_state_close(q1, qo, 1e-9, "q after births")
     assert_state_close(p1, po, 1e-8, "p after births")
-    np.testing.assert_allclose(g.V(q1, f_pos=True), m.V(q1, f_pos=True), rtol=1e-12)
-
-    g.Nsteps = 2
-    qm = g.reverse_format_q(zb["Q"][0, 0][:3 * 63])
-    np.random.seed(77)
-    g.run_RHMC(qm, f_pos=True, delta=1e-6, Niter=30, Nsteps=2, dt=0.05, N_max=120,
-               P_move=[0.6, 0.2, 0.2])
-    assert 63 - 30 <= g.N_chain.min() and g.N_chain.max() <= 63 + 30
-    assert np.isfinite(g.E_chain[g.A_chain]).all()
-    print("N_chain range %d..%d, moves %s, accepted %s" % (
-        g.N_chain.min(), g.N_chain.max(), np.bincount(g.move_chain, minlength=5),
-        np.bincount(g.move_chain[g.A_chain], minlength=5)))
+    Vg, Vo = g.V(q1, f_pos=True), m.V(q1, f_pos=True)
+    assert np.isfinite(Vo)
+    np.testing.assert_allclose(Vg, Vo, rtol=1e-12)

@@ -130,3 +130,49 @@ def test_c5_batch_invariance_determinism_segmentation(c5):
     for _ in range(5):
         qq, pp = ctx.leapfrog(P, qq, pp, wl.n_steps // 5)
     assert np.array_equal(qq, q) and np.array_equal(pp, p)
+
+
+@pytest.mark.parametrize("fused", [True, False])
+def test_c5_mh_f_pos_vs_oracle(gpu_lib, fused):
+    """run_RHMC's MH loop (sampler_RHMC.py:1018-1083) with the reference's
+    f_pos=True on the C5 geometry (256x256, K = 64, prior): rhmc_mh with host
+    draws from the C5 MH start (workloads.mh_start: every flux >= 1.5 f_lim,
+    so V is finite at the start), 2 chains x 3 iterations x 5 steps, against
+    the oracle's run_RHMC iterations — the four-kernel loop with its
+    wave-per-chain begin / end and the windowed pixel-major V(q') (no fused
+    MH kernel serves K = 64; the option must not matter).  Accepts exact,
+    chains 1e-9, energies 1e-11; the draws accept and reject."""
+    capi = gpu_lib
+    wl = workloads.make("C5", n_chains=2)
+    q0 = workloads.mh_start(wl)
+    assert np.isfinite(q0).all() and (q0[:, 0::3] >= 1.5 * wl.params["f_lim"]).all()
+    ctx = capi.Context(wl.D)
+    ctx.set_option(capi.OPT_MH_FUSED, int(fused))
+    P = capi.make_params(**wl.params)
+    m = _model(wl)
+    m.V_prior_const = wl.params["V_prior_const"]
+    n_iter, n_steps = 3, 5
+    rs = np.random.RandomState(5)
+    zz = rs.randn(n_iter, 2, q0.shape[1])
+    uu = rs.rand(n_iter, 2)
+    out = ctx.mh(P, q0, n_iter, n_steps, f_pos=True, z=zz, u=uu, record=True)
+    acc_all = []
+    for c in range(2):
+        q = q0[c].copy()
+        for it in range(n_iter):
+            Hd = m.H(q)
+            p = zz[it, c] * np.sqrt(Hd)
+            E0 = m.V(q, True) + m.T(p, Hd)
+            assert np.isfinite(E0)
+            np.testing.assert_allclose(out["E_chain"][it, c], E0, rtol=1e-11)
+            assert_state_close(out["q_chain"][it, c], q, 1e-9, "q_chain %d/%d" % (it, c))
+            q1, p1, _, _ = m.trajectory(q, p, n_steps, record=False)
+            dE = m.V(q1, True) + m.T(p1, m.H(q1)) - E0
+            a = bool((dE < 0) or (np.log(uu[it, c]) < -dE))
+            assert bool(out["accept"][it, c]) == a, (it, c, dE)
+            acc_all.append(a)
+            if a:
+                q = q1
+        assert_state_close(out["q"][c], q, 1e-9, "mh q chain %d" % c)
+    assert 0 < np.mean(acc_all) < 1, acc_all
+    ctx.close()

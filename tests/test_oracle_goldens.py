@@ -176,3 +176,55 @@ def test_c5_golden_reflects():
     z = load_golden("traj_c5")
     assert z["Q"].shape[:2] == (4, 51)
     assert (z["Q"][:, 1:, 0::3] < float(z["par_f_lim"])).any(axis=(1, 2)).all()
+
+
+def _mh_start(z, prefix):
+    par = R.params_from_npz(z, prefix + "par_")
+    q0 = z[prefix + "q_model"].copy()
+    q0[:, 0] = R.mag2flux(q0[:, 0]) * par["flux_to_count"]      # format_q (:209-217)
+    return par, q0.reshape(-1)
+
+
+@pytest.mark.parametrize("golden,name", [("mh", "mh1"), ("mh", "mh3"), ("mh_bigk", "d51"),
+                                         ("mh_bigk", "w64")])
+def test_run_RHMC_move0_replay(golden, name):
+    """multi_gym.run_RHMC with P_move = [1, 0, 0] restated (RefModel.run_mh)
+    on the reference's seeded stream reproduces the reference runs: the
+    accept sequence exactly, states and energies to a few ulp.  mh_bigk: many
+    stars with every start above the flux wall (d51: RHMC-big-sim4.py's
+    32x32 / 51-star geometry; w64: the C5 geometry, 256x256 / 64 stars), where
+    proposals are really accepted and rejected."""
+    z = load_golden(golden)
+    p = name + "/"
+    par, q0 = _mh_start(z, p)
+    m = R.RefModel(z[p + "D"], par)
+    n_it = int(z[p + "niter"]) + 1
+    o = m.run_mh(q0, np.random.RandomState(int(z[p + "seed"])), n_it, int(z[p + "nsteps"]))
+    A = z[p + "A_chain"].astype(bool)
+    np.testing.assert_array_equal(o["A_chain"], A)
+    if golden == "mh_bigk":
+        assert 0 < A.mean() < 1 and np.isfinite(z[p + "E_chain"]).all()
+    K3 = q0.size
+    np.testing.assert_allclose(o["q_chain"], z[p + "q_chain"][:, :K3], rtol=1e-13, atol=1e-13)
+    np.testing.assert_allclose(o["p_chain"], z[p + "p_chain"][:, :K3], rtol=1e-12, atol=1e-12)
+    for k in ("E_chain", "V_chain"):
+        np.testing.assert_allclose(o[k], z[p + k], rtol=1e-13)
+
+
+def test_rj_goldens_start_above_the_wall_and_jump():
+    """rj_big (64 model stars, births / splits past 64, RHMC-big-sim4.py's move
+    parameters) and flagship (RHMC-big-sim4.py as written, Niter 40): finite
+    energies, every move type proposed, jumps accepted, the chain past 64
+    stars in rj_big."""
+    z = load_golden("rj_big")
+    assert np.isfinite(z["b64/E_chain"]).all()
+    assert z["b64/N_chain"].max() > 65 and z["b64/N_chain"][0] == 64
+    assert 0 < z["b64/A_chain"].mean() < 1
+    assert (z["b64/beta_a"], z["b64/beta_b"], z["b64/K_split"]) == (4., 4., 1.)
+    f = load_golden("flagship")
+    assert np.isfinite(f["E_chain"]).all()
+    assert set(np.unique(f["move_chain"])) == {0, 1, 2, 3, 4}
+    acc = f["A_chain"].astype(bool)
+    assert set(np.unique(f["move_chain"][acc])) == {0, 1, 2, 3, 4}
+    assert f["N_chain"][0] == 5 and f["q_true"].shape == (51, 3)
+    assert list(f["P_move"]) == [0.6, 0.2, 0.2] and int(f["N_max"]) == 120

@@ -70,3 +70,21 @@ def test_rj_batched_equals_per_seed_runs(P_move, capsys):
     # the batch mixed star counts and both kinds of decision happened
     assert len(set(g.N_chain.ravel())) > 1
     assert g.A_chain.any() and not g.A_chain.all()
+
+
+def test_rj_batched_python_engine_takes_list_schedules():
+    """schedule_g_ff2 / schedule_beta as plain lists work on the NumPy loop as
+    on the native engine (both normalise them to arrays) and give the array
+    schedule's run."""
+    starts = [np.array([[18., 10.2, 12.7], [19., 20.3, 18.1]]),
+              np.array([[18.3, 10.5, 12.2]])]
+    kw = dict(f_pos=True, Niter=6, Nsteps=2, dt=0.05, N_max=6, P_move=[0.4, 0.3, 0.3])
+    a, b = _gym(), _gym()
+    a.run_RHMC_rj_batched([m.copy() for m in starts], [3, 4], engine="python",
+                          schedule_g_ff2=[1., 2., 4.], schedule_beta=[0.5], **kw)
+    b.run_RHMC_rj_batched([m.copy() for m in starts], [3, 4], engine="python",
+                          schedule_g_ff2=np.array([1., 2., 4.]), schedule_beta=np.array([0.5]),
+                          **kw)
+    for k in ("q_chain", "E_chain", "A_chain", "N_chain"):
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    assert a.g_ff2 == b.g_ff2 == 4.
