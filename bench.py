@@ -226,13 +226,20 @@ def source_hash(root=ROOT):
     return h.hexdigest()[:16]
 
 
-def load_pmc(workload, root=ROOT):
+def load_pmc(workload, n_chains=None, root=ROOT):
     """rocprofv3 PMC summary of the dominant kernel (profiles/pmc_<wl>.json,
     written by scripts/pmc_summary.py): HBM bytes per launch and executed
-    fp64 flops per chain-step.  Returns (summary, stale): a summary whose
-    `src_hash` is missing or differs from the shipped sources' is stale — its
-    counters describe other machine code, so roofline() reports no fraction."""
+    fp64 flops per chain-step.  A launch size with its own summary
+    (profiles/pmc_<wl>_<n_chains>.json: C5's 1024-chain share of 8 GPUs, whose
+    window split runs other code per chain-step) takes that one.  Returns
+    (summary, stale): a summary whose `src_hash` is missing or differs from
+    the shipped sources' is stale — its counters describe other machine code,
+    so roofline() reports no fraction."""
     path = os.path.join(root, "profiles", "pmc_%s.json" % workload.lower())
+    if n_chains is not None:
+        sized = os.path.join(root, "profiles", "pmc_%s_%d.json" % (workload.lower(), n_chains))
+        if os.path.exists(sized):
+            path = sized
     try:
         with open(path) as fh:
             pmc = json.load(fh)
@@ -424,6 +431,9 @@ def main():
                          "sampler_RHMC.py:303-309; the reference's default 1)")
     ap.add_argument("--mh-unfused", action="store_true",
                     help="--mode mh: the four-kernel loop (RHMC_OPT_MH_FUSED = 0)")
+    ap.add_argument("--window-split", type=int, choices=(0, 1, 2, 4), default=0,
+                    help="RHMC_OPT_WINDOW_SPLIT for the multi-star register-window kernel "
+                         "(0: by batch size; results bit-identical)")
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
     ap.add_argument("--n-real", type=int, default=1000)
     ap.add_argument("--dry-run", action="store_true",
@@ -502,6 +512,8 @@ def main():
     leap = args.leap or wl.n_steps
     P = capi.make_params(**wl.params)
     ctx = capi.Context(wl.D, device=gpu)
+    if args.window_split:
+        ctx.set_option(capi.OPT_WINDOW_SPLIT, args.window_split)
     q = torch.from_numpy(wl.q0).to(dev).contiguous()
     p = torch.from_numpy(wl.p0).to(dev).contiguous()
     it = torch.zeros((wl.n_chains, 2), dtype=torch.int32, device=dev)
@@ -600,7 +612,8 @@ def main():
     chain_steps = wl.n_chains * steps_per_launch
     value = total_chains * steps_per_launch * args.steps / wall
     # PMC summaries describe the implicit leapfrog kernel only
-    pmc, stale = load_pmc(wl.name) if args.mode == "leapfrog" else ({}, False)
+    pmc, stale = (load_pmc(wl.name, wl.n_chains) if args.mode == "leapfrog" and
+                  not args.window_split else ({}, False))
     metric = "chain-leapfrog-steps/sec, 48x48 1-star 4096 chains, 1/2/4/8 MI355X"
     if wl.name != "C2" or args.chains or args.global_chains or args.mode != "leapfrog":
         # not the headline configuration: name what was run

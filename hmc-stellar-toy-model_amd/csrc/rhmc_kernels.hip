@@ -38,6 +38,7 @@
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 #include "rhmc_dense.hpp"
+#include "rhmc_rows.hpp"
 
 namespace rhmc {
 
@@ -186,7 +187,23 @@ struct LeapArgs {
   int K, n_steps;
   Geometry g;
   Consts c;
+  // ragged sets (rhmc_leapfrog_ragged_device, the slotted kernels only): chain
+  // i is row rows[i] (NULL: row i) of [*][ld] arrays with Kc[row] stars; K is
+  // then the largest star count of the launch (it sizes LDS).  Kc NULL: every
+  // chain has K stars in rows of 3K.
+  const int32_t* Kc = nullptr;
+  const int64_t* rows = nullptr;
+  int64_t ld = 0;
 };
+
+// Row, star count and row stride of launch chain i (LeapArgs / EnergyArgs).
+template <class A>
+__device__ __forceinline__ void chain_row(const A& a, int64_t i, int64_t& row, int& K,
+                                          int64_t& ld) {
+  row = a.rows ? a.rows[i] : i;
+  K = a.Kc ? a.Kc[row] : a.K;
+  ld = a.Kc ? a.ld : 3 * (int64_t)K;
+}
 
 // Stage D into LDS (coalesced, whole workgroup) and return this wave's chain.
 __device__ __forceinline__ int64_t stage_image(double* sD, const double* __restrict__ D,
@@ -358,14 +375,15 @@ struct WinState {
 };
 
 // Lanes without a star in a slot carry a copy of star 0 (finite, never read).
+// The chain's stars start at element row * ld of q and p.
 template <int SLOTS>
-__device__ __forceinline__ void win_load(const LeapArgs& a, int64_t chain, int K,
+__device__ __forceinline__ void win_load(const LeapArgs& a, int64_t row, int64_t ld, int K,
                                          WinState<SLOTS>& s) {
   const int lane = lane_id();
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
     s.own[t] = kWave * t + lane < K;
-    const int64_t e = chain * 3 * (int64_t)K + 3 * (s.own[t] ? kWave * t + lane : 0);
+    const int64_t e = row * ld + 3 * (s.own[t] ? kWave * t + lane : 0);
     s.f[t] = a.q[e];
     s.x[t] = a.q[e + 1];
     s.y[t] = a.q[e + 2];
@@ -376,9 +394,9 @@ __device__ __forceinline__ void win_load(const LeapArgs& a, int64_t chain, int K
 }
 
 template <int SLOTS>
-__device__ __forceinline__ void win_store(const LeapArgs& a, int64_t chain, int K,
-                                          const WinState<SLOTS>& s, int it_p, int it_q,
-                                          unsigned st) {
+__device__ __forceinline__ void win_store(const LeapArgs& a, int64_t chain, int64_t row,
+                                          int64_t ld, int K, const WinState<SLOTS>& s, int it_p,
+                                          int it_q, unsigned st) {
   const int lane = lane_id();
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
@@ -386,7 +404,7 @@ __device__ __forceinline__ void win_store(const LeapArgs& a, int64_t chain, int 
     if (!(isfinite(s.f[t]) && isfinite(s.x[t]) && isfinite(s.y[t]) && isfinite(s.pf[t]) &&
           isfinite(s.px[t]) && isfinite(s.py[t])))
       st |= RHMC_STATUS_NONFINITE;
-    const int64_t e = chain * 3 * (int64_t)K + 3 * (kWave * t + lane);
+    const int64_t e = row * ld + 3 * (kWave * t + lane);
     a.q[e] = s.f[t];
     a.q[e + 1] = s.x[t];
     a.q[e + 2] = s.y[t];
@@ -528,10 +546,12 @@ __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
-  const int K = a.K;
+  int64_t row, ld;
+  int K;
+  chain_row(a, chain, row, K, ld);
   const LeanConsts lc = lean_consts(c);
   WinState<SLOTS> s;
-  win_load<SLOTS>(a, chain, K, s);
+  win_load<SLOTS>(a, row, ld, K, s);
   int it_p = 0, it_q = 0;
   unsigned st = 0u;
   const int rows = a.g.rows, cols = a.g.cols;
@@ -541,7 +561,7 @@ __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
           double(&gf)[SLOTS], double(&gx)[SLOTS], double(&gy)[SLOTS]) {
         G::template gradient<SLOTS>(gctx, K, f, x, y, c, lc, true, gf, gx, gy);
       });
-  win_store<SLOTS>(a, chain, K, s, it_p, it_q, st);
+  win_store<SLOTS>(a, chain, row, ld, K, s, it_p, it_q, st);
 }
 
 struct GradArgs {
@@ -585,6 +605,10 @@ struct EnergyArgs {
   int K, f_pos;
   Geometry g;
   Consts c;
+  // ragged sets (rhmc_energy_ragged_device, slotted kernels only), as LeapArgs
+  const int32_t* Kc = nullptr;
+  const int64_t* rows = nullptr;
+  int64_t ld = 0;
 };
 
 // V (sampler_RHMC.py:294-351) and T at H(q) (:353-363), one wave per chain.
@@ -696,7 +720,7 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
   const int K = a.K;
   const LeanConsts lc = lean_consts(c);
   WinState<SLOTS> s;
-  win_load<SLOTS>(a, chain, K, s);
+  win_load<SLOTS>(a, chain, 3 * (int64_t)K, K, s);
   const double dt = c.dt;
   unsigned st = 0u;
   double gf[SLOTS], gx[SLOTS], gy[SLOTS];
@@ -770,7 +794,7 @@ __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_po
       }
     }
   }
-  win_store<SLOTS>(a, chain, K, s, 0, 0, st);
+  win_store<SLOTS>(a, chain, chain, 3 * (int64_t)K, K, s, 0, 0, st);
 }
 
 // samplers.lightsource_gym.HMC_random's trajectory (samplers.py:519-552):
@@ -796,7 +820,7 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
   const LeanConsts lc = lean_consts(c);
   const int lane = lane_id();
   WinState<SLOTS> s;
-  win_load<SLOTS>(a, chain, K, s);
+  win_load<SLOTS>(a, chain, 3 * (int64_t)K, K, s);
   double dtf[SLOTS], dtx[SLOTS], dty[SLOTS];
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
@@ -851,18 +875,18 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
       s.py[t] = hy[t] + dty[t] * gy[t] / 2.0;
     }
   }
-  win_store<SLOTS>(a, chain, K, s, 0, 0, st);
+  win_store<SLOTS>(a, chain, chain, 3 * (int64_t)K, K, s, 0, 0, st);
 }
 
 // Star 64 t + lane's (f, x, y) of a chain (lanes without a star: star 0's).
 template <int SLOTS>
-__device__ __forceinline__ void win_load_q(const double* q, int64_t chain, int K,
+__device__ __forceinline__ void win_load_q(const double* q, int64_t row, int64_t ld, int K,
                                            double (&f)[SLOTS], double (&x)[SLOTS],
                                            double (&y)[SLOTS], bool (&own)[SLOTS]) {
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
     own[t] = win_own(t, K);
-    const int64_t e = chain * 3 * (int64_t)K + 3 * (own[t] ? kWave * t + lane_id() : 0);
+    const int64_t e = row * ld + 3 * (own[t] ? kWave * t + lane_id() : 0);
     f[t] = q[e];
     x[t] = q[e + 1];
     y[t] = q[e + 2];
@@ -881,7 +905,7 @@ __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   const LeanConsts lc = lean_consts(a.c);
   double f[SLOTS], x[SLOTS], y[SLOTS], gf[SLOTS], gx[SLOTS], gy[SLOTS];
   bool own[SLOTS];
-  win_load_q<SLOTS>(a.q, chain, K, f, x, y, own);
+  win_load_q<SLOTS>(a.q, chain, 3 * (int64_t)K, K, f, x, y, own);
   G::template gradient<SLOTS>(gctx, K, f, x, y, a.c, lc, a.with_metric != 0, gf, gx, gy);
 #pragma unroll
   for (int t = 0; t < SLOTS; ++t) {
@@ -904,17 +928,19 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
   const int lane = lane_id();
-  const int K = a.K;
+  int64_t row, ld;
+  int K;
+  chain_row(a, chain, row, K, ld);
   const LeanConsts lc = lean_consts(c);
   double f[SLOTS], x[SLOTS], y[SLOTS];
   bool own[SLOTS];
-  win_load_q<SLOTS>(a.q, chain, K, f, x, y, own);
+  win_load_q<SLOTS>(a.q, row, ld, K, f, x, y, own);
   if (a.T) {
     double t1 = 0.0, t2 = 0.0;
 #pragma unroll
     for (int t = 0; t < SLOTS; ++t) {
       if (!own[t]) continue;
-      const int64_t e = chain * 3 * (int64_t)K + 3 * (kWave * t + lane);
+      const int64_t e = row * ld + 3 * (kWave * t + lane);
       const double pf = a.p[e], px = a.p[e + 1], py = a.p[e + 2];
       const double hff = H_ff(f[t], c), hxx = H_xx(f[t], c);
       t1 += pf * pf / hff + px * px / hxx + py * py / hxx;
@@ -1661,6 +1687,123 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
                     int64_t n_chains, int32_t K, int32_t n_steps, int32_t* d_it, int32_t* d_st,
                     hipStream_t s);
 
+// ---------------------------------------------------------------------------
+// Ragged chain sets (rhmc.h: rhmc_leapfrog_ragged_device & co.; the
+// reversible-jump driver).  Which star counts the automatic dispatch serves
+// with a slotted one-wave-per-chain kernel — for both the step and the
+// energy — where chains of different K can share a launch: 1 = the dense
+// kernel (32/48-px images, from 11 stars), 2 = the windowed kernel; 0 = a
+// kernel with a fixed K per launch (one-star, pixel-major, multi-star
+// register-window, the LDS-image generic kernels).
+int ragged_family(const rhmc_ctx* ctx, const Consts& c, int K) {
+  if (K < 1 || K > kMaxK) return 0;
+  if (dense_path(ctx, K, c)) return 1;
+  if (K == 1) return 0;
+  if (use_pixk(ctx, K, c) || use_tiledrk(ctx, K, c)) return 0;
+  return use_windowed(ctx, K) && window_exact(c) ? 2 : 0;
+}
+
+// [K_min, K_max]: one family and one register-slot count (the launch's SLOTS
+// and LDS follow K_max)
+int ragged_check(const rhmc_ctx* ctx, const Consts& c, int K_min, int K_max, int64_t ld,
+                 int* family) {
+  if (K_min < 1 || K_max > kMaxK || K_min > K_max)
+    return fail(RHMC_ERR_ARG, "ragged set: need 1 <= K_min <= K_max <= 256");
+  if (win_slots(K_min) != win_slots(K_max))
+    return fail(RHMC_ERR_ARG, "ragged set: K_min and K_max need the same register slots "
+                              "(1-64, 65-128, 129-256 stars)");
+  if (ld < 3 * (int64_t)K_max) return fail(RHMC_ERR_ARG, "ragged set: ld < 3 K_max");
+  const int f = ragged_family(ctx, c, K_min);
+  for (int K = K_min; K <= K_max; ++K)
+    if (ragged_family(ctx, c, K) != f || f == 0)
+      return fail(RHMC_ERR_UNSUPPORTED, "ragged set: K = " + std::to_string(K) +
+                                            " is not served by a slotted kernel on this image "
+                                            "(rhmc_ragged_ok)");
+  *family = f;
+  return RHMC_OK;
+}
+
+int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                           int64_t ld, const int64_t* d_rows, const int32_t* d_K, int64_t n,
+                           int K_min, int K_max, int32_t n_steps, hipStream_t s) {
+  LeapArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  if (n_steps < 0) return fail(RHMC_ERR_ARG, "n_steps < 0");
+  if (P->counter_max < 1) return fail(RHMC_ERR_ARG, "counter_max < 1");
+  int fam;
+  if ((rc = ragged_check(ctx, a.c, K_min, K_max, ld, &fam))) return rc;
+  if (n == 0) return RHMC_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int path = dense_path(ctx, K_max, a.c);
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  a.q = d_q;
+  a.p = d_p;
+  a.fp_iters = nullptr;
+  a.status = nullptr;
+  a.D = ctx->d_D;
+  a.n_chains = n;
+  a.K = K_max;
+  a.n_steps = n_steps;
+  a.Kc = d_K;
+  a.rows = d_rows;
+  a.ld = ld;
+  size_t lds;
+  int W;
+  if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
+  const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+  return with_path(path, K_max, [&](auto gt, auto st) {
+    using G = typename decltype(gt)::type;
+    hipLaunchKernelGGL((leapfrog_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return (int)RHMC_OK;
+  });
+}
+
+int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int64_t ld,
+                         const int64_t* d_rows, const int32_t* d_K, int64_t n, int K_min,
+                         int K_max, int f_pos, double* d_V, hipStream_t s) {
+  EnergyArgs a;
+  int rc = make_consts(P, &a.c);
+  if (rc) return rc;
+  int fam;
+  if ((rc = ragged_check(ctx, a.c, K_min, K_max, ld, &fam))) return rc;
+  if (n == 0) return RHMC_OK;
+  HIP_TRY(hipSetDevice(ctx->device));
+  const int path = dense_path(ctx, K_max, a.c);
+  size_t lds;
+  int W;
+  if (path) {
+    if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
+  } else {  // potential-only windowed tables, as launch_energy
+    W = 4;
+    while (W > 1 && WinEG::lds_bytes(W, K_max) > (size_t)ctx->max_lds) W >>= 1;
+    lds = WinEG::lds_bytes(W, K_max);
+    if (lds > (size_t)ctx->max_lds)
+      return fail(RHMC_ERR_UNSUPPORTED, "windowed energy tables exceed the device's LDS");
+  }
+  a.q = d_q;
+  a.p = nullptr;
+  a.V = d_V;
+  a.T = nullptr;
+  a.D = ctx->d_D;
+  a.n_chains = n;
+  a.K = K_max;
+  a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
+  a.g = make_geometry(ctx->rows, ctx->cols);
+  a.Kc = d_K;
+  a.rows = d_rows;
+  a.ld = ld;
+  const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+  auto go = [&](auto gt, auto st) {
+    using G = typename decltype(gt)::type;
+    hipLaunchKernelGGL((energy_win_kernel<G, decltype(st)::value>), grid, block, lds, s, a);
+    HIP_TRY(hipGetLastError());
+    return (int)RHMC_OK;
+  };
+  return path ? with_path(path, K_max, go) : with_slots<WinEG>(K_max, go);
+}
+
 // One star where launch_leapfrog takes the register-window kernel (28-px
 // window, 32/48/64-px image, fewer chains than the lane-group threshold): the
 // whole MH loop in one launch (rhmc_mhk1.hpp).  RHMC_OPT_MH_FUSED = 0, or a
@@ -2342,6 +2485,90 @@ int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, doubl
   if (n_chains > 0 && (!d_q || !d_p)) return fail(RHMC_ERR_ARG, "q/p is NULL");
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   return launch_leapfrog(ctx, P, d_q, d_p, n_chains, K, n_steps, d_fp_iters, d_status, s);
+}
+
+int rhmc_ragged_ok(rhmc_ctx* ctx, const rhmc_params* P, int32_t K, int32_t* ok) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!ok) return fail(RHMC_ERR_ARG, "ok is NULL");
+  if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
+  Consts c;
+  if (int rc = make_consts(P, &c)) return rc;
+  *ok = ragged_family(ctx, c, K) != 0 ? 1 : 0;
+  return RHMC_OK;
+}
+
+int rhmc_leapfrog_ragged_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                                int64_t ld, const int64_t* d_rows, const int32_t* d_K,
+                                int64_t n, int32_t K_min, int32_t K_max, int32_t n_steps,
+                                void* stream) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
+  if (n < 0 || n > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "bad n");
+  if (n > 0 && (!d_q || !d_p || !d_K)) return fail(RHMC_ERR_ARG, "q, p or K is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_leapfrog_ragged(ctx, P, d_q, d_p, ld, d_rows, d_K, n, K_min, K_max, n_steps, s);
+}
+
+int rhmc_energy_ragged_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int64_t ld,
+                              const int64_t* d_rows, const int32_t* d_K, int64_t n,
+                              int32_t K_min, int32_t K_max, int32_t f_pos, double* d_V,
+                              void* stream) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
+  if (n < 0 || n > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "bad n");
+  if (n > 0 && (!d_q || !d_K || !d_V)) return fail(RHMC_ERR_ARG, "q, K or V is NULL");
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  return launch_energy_ragged(ctx, P, d_q, ld, d_rows, d_K, n, K_min, K_max, f_pos, d_V, s);
+}
+
+int rhmc_rows_copy_device(rhmc_ctx* ctx, const double* d_src, int64_t ld_src,
+                          const int64_t* d_src_rows, double* d_dst, int64_t ld_dst,
+                          const int64_t* d_dst_rows, int64_t n, int32_t width, void* stream) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (n < 0 || width < 0 || ld_src < width || ld_dst < width)
+    return fail(RHMC_ERR_ARG, "rows copy: need n, width >= 0 and ld_src, ld_dst >= width");
+  if (n == 0 || width == 0) return RHMC_OK;
+  if (!d_src || !d_dst) return fail(RHMC_ERR_ARG, "rows copy: src or dst is NULL");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  RowsCopyArgs a{d_src, d_dst, d_src_rows, d_dst_rows, ld_src, ld_dst, n, width};
+  const int64_t total = n * (int64_t)width;
+  hipLaunchKernelGGL(rows_copy_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
+}
+
+int rhmc_kinetic_rows_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, double* d_p,
+                             int64_t ld, const int32_t* d_K, const double* d_z,
+                             const int64_t* d_zoff, int64_t n, double* d_T, void* stream) {
+  if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+  if (!P) return fail(RHMC_ERR_ARG, "params is NULL");
+  if (n < 0 || ld < 3) return fail(RHMC_ERR_ARG, "kinetic: bad n or ld");
+  if (n == 0) return RHMC_OK;
+  if (!d_q || !d_p || !d_K || !d_T || (d_z && !d_zoff))
+    return fail(RHMC_ERR_ARG, "kinetic: q, p, K, T (or zoff with z) is NULL");
+  HIP_TRY(hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  KineticArgs a;
+  a.q = d_q;
+  a.p = d_p;
+  a.z = d_z;
+  a.zoff = d_zoff;
+  a.K = d_K;
+  a.T = d_T;
+  a.ld = ld;
+  a.n = n;
+  a.g_ff2 = P->g_ff2;
+  a.g_ff = P->g_ff;
+  a.g_xx = P->g_xx;
+  a.g0 = P->g0;
+  a.g1 = P->g1;
+  a.g2 = P->g2;
+  a.B = P->B_count;
+  a.f_low = P->f_low;
+  hipLaunchKernelGGL(kinetic_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, a);
+  HIP_TRY(hipGetLastError());
+  return RHMC_OK;
 }
 
 int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p, int64_t n_chains,

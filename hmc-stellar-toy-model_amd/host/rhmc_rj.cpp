@@ -265,7 +265,6 @@ struct Run {
   }
 
   int energies(const std::vector<int64_t>& idx, std::vector<double>& V) {
-    if (staged.energy) return energies_staged(idx, V);
     std::vector<double> qb, vb;
     for (auto& grp : groups(idx)) {
       const int32_t K = grp.first;
@@ -282,60 +281,7 @@ struct Run {
     return 0;
   }
 
-  // optional (the context path): a phase's groups staged in one pinned buffer
-  // and run concurrently on several HIP streams.  buffer(user, doubles)
-  // returns the staging area; launch(...) runs group g from q at off[g] and
-  // p at off[g] + n[g] 3 K[g], in place.
-  struct Staged {
-    void* user = nullptr;
-    double* (*buffer)(void* user, size_t doubles) = nullptr;
-    int (*launch)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
-                  const int64_t* n, const size_t* off, int32_t n_steps) = nullptr;
-    // V of group g: q at off[g], V written at off[g] + n[g] 3 K[g]
-    int (*energy)(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
-                  const int64_t* n, const size_t* off, int32_t f_pos) = nullptr;
-  };
-  Staged staged;
-
-  int energies_staged(const std::vector<int64_t>& idx, std::vector<double>& V) {
-    const auto gs = groups(idx);
-    if (gs.empty()) return 0;
-    const int32_t G = (int32_t)gs.size();
-    std::vector<int32_t> Ks((size_t)G);
-    std::vector<int64_t> ns((size_t)G);
-    std::vector<size_t> off((size_t)G);
-    size_t total = 0;
-    for (int32_t g = 0; g < G; ++g) {
-      Ks[g] = gs[g].first;
-      ns[g] = (int64_t)gs[g].second.size();
-      off[g] = total;
-      total += (size_t)ns[g] * (3 * (size_t)Ks[g] + 1);
-    }
-    double* h = staged.buffer(staged.user, total);
-    if (!h) return fail(RHMC_ERR_NOMEM, "staging buffer: " + g_err);
-    std::vector<int64_t> slots, slot_c;
-    std::vector<double*> slot_q, slot_v;
-    for (int32_t g = 0; g < G; ++g) {
-      const size_t d = 3 * (size_t)Ks[g];
-      for (size_t i = 0; i < gs[g].second.size(); ++i) {
-        slots.push_back((int64_t)slots.size());
-        slot_c.push_back(gs[g].second[i]);
-        slot_q.push_back(h + off[g] + i * d);
-        slot_v.push_back(h + off[g] + (size_t)ns[g] * d + i);
-      }
-    }
-    parallel(slots, [&](int64_t j) {
-      const Chain& c = ch[slot_c[j]];
-      std::memcpy(slot_q[j], c.q.data(), c.q.size() * 8);
-    });
-    const int rc = staged.energy(staged.user, &P, G, Ks.data(), ns.data(), off.data(), cfg->f_pos);
-    if (rc != 0) return engine_fail(rc, "energy");
-    for (size_t j = 0; j < slots.size(); ++j) V[slot_c[j]] = *slot_v[j];
-    return 0;
-  }
-
   int trajectories(const std::vector<int64_t>& idx) {
-    if (staged.launch) return trajectories_staged(idx);
     std::vector<double> qb, pb;
     for (auto& grp : groups(idx)) {
       const int32_t K = grp.first;
@@ -355,52 +301,6 @@ struct Run {
         std::memcpy(ch[cs[i]].p.data(), &pb[i * d], d * 8);
       }
     }
-    return 0;
-  }
-
-  int trajectories_staged(const std::vector<int64_t>& idx) {
-    const auto gs = groups(idx);
-    if (gs.empty()) return 0;
-    const int32_t G = (int32_t)gs.size();
-    std::vector<int32_t> Ks((size_t)G);
-    std::vector<int64_t> ns((size_t)G);
-    std::vector<size_t> off((size_t)G);
-    size_t total = 0;
-    for (int32_t g = 0; g < G; ++g) {
-      Ks[g] = gs[g].first;
-      ns[g] = (int64_t)gs[g].second.size();
-      off[g] = total;
-      total += 2 * (size_t)ns[g] * 3 * (size_t)Ks[g];
-    }
-    double* h = staged.buffer(staged.user, total);
-    if (!h) return fail(RHMC_ERR_NOMEM, "staging buffer: " + g_err);
-    // slot j of the phase: its chain, its q row and the offset of its p row
-    // (group g's p block follows its q block) in the staging buffer
-    std::vector<int64_t> slots, slot_c;
-    std::vector<double*> slot_q;
-    std::vector<size_t> pofs;
-    for (int32_t g = 0; g < G; ++g) {
-      const size_t d = 3 * (size_t)Ks[g];
-      for (size_t i = 0; i < gs[g].second.size(); ++i) {
-        slots.push_back((int64_t)slots.size());
-        slot_c.push_back(gs[g].second[i]);
-        slot_q.push_back(h + off[g] + i * d);
-        pofs.push_back((size_t)ns[g] * d);
-      }
-    }
-    parallel(slots, [&](int64_t j) {
-      const Chain& c = ch[slot_c[j]];
-      std::memcpy(slot_q[j], c.q.data(), c.q.size() * 8);
-      std::memcpy(slot_q[j] + pofs[j], c.p.data(), c.p.size() * 8);
-    });
-    const int rc = staged.launch(staged.user, &P, G, Ks.data(), ns.data(), off.data(),
-                                 cfg->n_steps);
-    if (rc != 0) return engine_fail(rc, "steps");
-    parallel(slots, [&](int64_t j) {
-      Chain& c = ch[slot_c[j]];
-      std::memcpy(c.q.data(), slot_q[j], c.q.size() * 8);
-      std::memcpy(c.p.data(), slot_q[j] + pofs[j], c.p.size() * 8);
-    });
     return 0;
   }
 
@@ -585,14 +485,13 @@ int host_threads(const rhmc_rj_config* cfg) {
 // n chains (a contiguous slice of the caller's: q, K, seeds point at its
 // first chain); record row l of chain c is l * rec_stride + rec_off + c; nt
 // host threads; the phase times are added to phase_out[7].
-int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_params* P0,
+int run(const rhmc_rj_physics* phys, const rhmc_params* P0,
         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
         const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
         double* phase_out) {
   if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
   Run R;
   R.phys = phys;
-  if (staged) R.staged = *staged;
   R.P = *P0;
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
@@ -771,41 +670,26 @@ int run(const rhmc_rj_physics* phys, const Run::Staged* staged, const rhmc_param
   return 0;
 }
 
-// the engine as physics: V by rhmc_energy; the trajectories of all star-count
-// groups of a phase at once, each group on one of kStreams HIP streams
-// (rhmc_leapfrog_device), so that small groups fill the GPU together instead
-// of one after the other
-constexpr int kStreams = 4;
-static_assert(kStreams >= kMaxPipes, "a stream per pipe at least");
-
-// The streams live for the process, kStreams per device, created on first use
-// and warmed by one small copy each: the first dispatch to a new HIP stream
-// binds its hardware queue, which cost 6-11 ms per stream when it happened
-// inside a run (profiles/r04_rj/).
-struct DeviceStreams {
-  hipStream_t s[kStreams] = {};
-  double* warm = nullptr;
-};
-
-std::mutex g_streams_mu;
-std::map<int, DeviceStreams> g_streams;
-
-struct CtxEngine {
-  rhmc_ctx* ctx = nullptr;
-  hipStream_t s[kStreams] = {};
-  int ns = kStreams;             // streams in use: s[0 .. ns)
-  int dev = 0;
-  double* d = nullptr;
-  size_t d_bytes = 0;
-  double* h = nullptr;
-  size_t h_bytes = 0;
-  ~CtxEngine() {  // nothing may still be copying into the buffers (error paths)
-    for (int i = 0; i < ns; ++i)
-      if (s[i]) (void)hipStreamSynchronize(s[i]);
-    if (d) (void)hipFree(d);
-    if (h) (void)hipHostFree(h);
-  }
-};
+// ===================================================================== device
+// rhmc_rj_run: the chains live in HBM for the whole run (librhmc.so's
+// ragged-set entry points, rhmc.h ABI 4).  Per pipe: padded [n][W] rows
+// (W = 3 N_max, zeros past a chain's 3 K) of
+//   Q0   the chains' states (the iteration's starting point; the q_chain rows)
+//   Q, P the working trajectory state
+// and per iteration only these cross PCIe:
+//   H2D  the host-drawn normals z (3 K per chain: the NumPy-stream draws stay
+//        on the host, bit for bit), the star counts, index lists, and the
+//        jumping chains' proposed rows
+//   D2H  T0, V / T at the end (one double each per chain), the jumping chains'
+//        rows before their proposal, and — when the caller records them — the
+//        q_chain / p_chain rows (on a second stream, overlapping the trajectory)
+// The momentum p = z sqrt(H(q)) and both kinetic energies run on the device
+// (rhmc_kinetic_rows_device, the reference's operation order); every phase is
+// one ragged launch for the star counts the slotted kernels serve (dense /
+// windowed, rhmc_ragged_ok) plus one packed launch per remaining star count
+// (the one-star, pixel-major and multi-star register-window kernels), the
+// packed ones spread over the pipe's two streams.
+constexpr int kStreamsPerPipe = 2;  // main (in order) + aux (records, packed groups)
 
 #define RJ_HIP(expr)                                                                   \
   do {                                                                                 \
@@ -814,137 +698,526 @@ struct CtxEngine {
                                                         hipGetErrorString(e_));        \
   } while (0)
 
-int engine_init(CtxEngine& E) {
-  const double* dimg = nullptr;
-  if (int rc = rhmc_ctx_image_device(E.ctx, &dimg)) return rc;
-  if (!dimg) return fail(RHMC_ERR_ARG, "context has no image");
-  hipPointerAttribute_t at;
-  RJ_HIP(hipPointerGetAttributes(&at, dimg));
-  RJ_HIP(hipSetDevice(at.device));
-  E.dev = at.device;
-  std::lock_guard<std::mutex> lock(g_streams_mu);
-  DeviceStreams& ds = g_streams[at.device];
-  if (!ds.warm) {
-    RJ_HIP(hipMalloc(&ds.warm, kStreams * sizeof(double)));
-    for (int i = 0; i < kStreams; ++i) {
-      RJ_HIP(hipStreamCreateWithFlags(&ds.s[i], hipStreamNonBlocking));
-      RJ_HIP(hipMemsetAsync(ds.warm + i, 0, sizeof(double), ds.s[i]));
-    }
-    for (int i = 0; i < kStreams; ++i) RJ_HIP(hipStreamSynchronize(ds.s[i]));
+#define RJ_TRY(expr)                        \
+  do {                                      \
+    if (int rc_ = (expr)) return rc_;       \
+  } while (0)
+
+// Index lists of an iteration, one region each (an async copy reads its pinned
+// source when it executes, so no region is rewritten before a sync).
+enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions };
+
+// One pipe's buffers: device rows and pinned staging, grown as needed and kept
+// for the process (a run of 4,096 chains at N_max 120 holds ~90 MB of HBM and
+// ~60 MB of pinned memory per pipe).  `mu` is held for a whole run, so two
+// concurrent rhmc_rj_run calls on one device serialise pipe by pipe.
+struct Work {
+  std::mutex mu;
+  int dev = -1;
+  hipStream_t s[kStreamsPerPipe] = {};
+  hipEvent_t ev[4] = {};
+  int64_t cap_n = 0, cap_W = 0;
+  // device
+  double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *Ps = nullptr, *Z = nullptr, *J = nullptr;
+  double *pack = nullptr, *T0 = nullptr, *T1 = nullptr, *V = nullptr;
+  int32_t* Kd = nullptr;
+  int64_t *zoffd = nullptr, *idxd = nullptr;
+  // pinned host
+  double *Zh = nullptr, *Jh = nullptr, *recq = nullptr, *recp = nullptr;
+  double *T0h = nullptr, *T1h = nullptr, *Vh = nullptr;
+  int32_t* Kh = nullptr;
+  int64_t *zoffh = nullptr, *idxh = nullptr;
+
+  void release() {
+    for (double* d : {Q, P, Q0, Ps, Z, J, pack, T0, T1, V}) (void)hipFree(d);
+    (void)hipFree(Kd);
+    (void)hipFree(zoffd);
+    (void)hipFree(idxd);
+    for (double* h : {Zh, Jh, recq, recp, T0h, T1h, Vh}) (void)hipHostFree(h);
+    (void)hipHostFree(Kh);
+    (void)hipHostFree(zoffh);
+    (void)hipHostFree(idxh);
+    Q = P = Q0 = Ps = Z = J = pack = T0 = T1 = V = nullptr;
+    Kd = nullptr;
+    zoffd = idxd = nullptr;
+    Zh = Jh = recq = recp = T0h = T1h = Vh = nullptr;
+    Kh = nullptr;
+    zoffh = idxh = nullptr;
+    cap_n = cap_W = 0;
   }
-  for (int i = 0; i < kStreams; ++i) E.s[i] = ds.s[i];
+
+  // streams and events on `device` once; buffers for n chains of W doubles
+  int ensure(int device, int64_t n, int64_t W) {
+    if (dev < 0) {
+      dev = device;
+      for (auto& st : s) RJ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      for (auto& e : ev) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    }
+    if (n <= cap_n && W <= cap_W) return 0;
+    for (auto& st : s) RJ_HIP(hipStreamSynchronize(st));
+    release();
+    const int64_t N = std::max<int64_t>(n, 1), M = N * W;
+    auto dmal = [](auto** p, size_t count) {
+      return hipMalloc((void**)p, count * sizeof(**p)) == hipSuccess;
+    };
+    auto hmal = [](auto** p, size_t count) {
+      return hipHostMalloc((void**)p, count * sizeof(**p), hipHostMallocDefault) == hipSuccess;
+    };
+    const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&Ps, M) && dmal(&Z, M) &&
+                    dmal(&J, 2 * M) && dmal(&pack, 4 * M) && dmal(&T0, N) && dmal(&T1, N) &&
+                    dmal(&V, N) && dmal(&Kd, N) && dmal(&zoffd, N) &&
+                    dmal(&idxd, kIdxRegions * N) && hmal(&Zh, M) && hmal(&Jh, 2 * M) &&
+                    hmal(&recq, M) && hmal(&recp, M) && hmal(&T0h, N) && hmal(&T1h, N) &&
+                    hmal(&Vh, N) && hmal(&Kh, N) && hmal(&zoffh, N) &&
+                    hmal(&idxh, kIdxRegions * N);
+    if (!ok) {
+      release();
+      return fail(RHMC_ERR_NOMEM, "reversible-jump device buffers: allocation failed");
+    }
+    cap_n = N;
+    cap_W = W;
+    return 0;
+  }
+};
+
+std::mutex g_work_mu;
+std::map<std::pair<int, int>, Work*> g_work;  // (device, pipe), process lifetime
+
+Work* work_for(int dev, int pipe) {
+  std::lock_guard<std::mutex> lock(g_work_mu);
+  Work*& w = g_work[{dev, pipe}];
+  if (!w) w = new Work();
+  return w;
+}
+
+// The caller's current device, restored when a run returns.
+struct DeviceGuard {
+  int prev = -1;
+  DeviceGuard() {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// One phase's launch plan over chains `idx` (star counts K): the chains of the
+// slotted kernels' star counts grouped by register slots (one ragged launch
+// each), then one packed launch per other star count (first appearance).
+struct Call {
+  bool ragged;
+  int32_t Kmin, Kmax;
+  int64_t off, n;  // the call's chains: order[off .. off + n)
+};
+struct Plan {
+  std::vector<int64_t> order;
+  std::vector<Call> calls;
+};
+
+Plan make_plan(const std::vector<int64_t>& idx, const std::vector<int32_t>& K,
+               const std::vector<char>& ragged_ok) {
+  Plan pl;
+  std::vector<int64_t> cls[3];
+  std::vector<std::pair<int32_t, std::vector<int64_t>>> groups;
+  std::map<int32_t, size_t> where;
+  for (int64_t c : idx) {
+    const int32_t k = K[c];
+    if (ragged_ok[k]) {
+      cls[k <= 64 ? 0 : k <= 128 ? 1 : 2].push_back(c);
+      continue;
+    }
+    auto it = where.find(k);
+    if (it == where.end()) {
+      where[k] = groups.size();
+      groups.push_back({k, {c}});
+    } else {
+      groups[it->second].second.push_back(c);
+    }
+  }
+  for (auto& v : cls) {
+    if (v.empty()) continue;
+    int32_t lo = 256, hi = 1;
+    for (int64_t c : v) {
+      lo = std::min(lo, K[c]);
+      hi = std::max(hi, K[c]);
+    }
+    pl.calls.push_back({true, lo, hi, (int64_t)pl.order.size(), (int64_t)v.size()});
+    pl.order.insert(pl.order.end(), v.begin(), v.end());
+  }
+  for (auto& g : groups) {
+    pl.calls.push_back({false, g.first, g.first, (int64_t)pl.order.size(),
+                        (int64_t)g.second.size()});
+    pl.order.insert(pl.order.end(), g.second.begin(), g.second.end());
+  }
+  return pl;
+}
+
+struct DevRun {
+  rhmc_ctx* ctx;
+  Work* w;
+  int64_t n, W;
+  std::vector<int32_t>& K;  // host star counts (mirrored to w->Kd by upload_K)
+  const std::vector<char>& ragged_ok;
+
+  int engine_fail(int rc, const char* what) {
+    const char* m = rhmc_last_error();
+    return fail(rc, std::string("engine ") + what + " failed: " + (m ? m : ""));
+  }
+  int upload_K() {
+    std::copy(K.begin(), K.end(), w->Kh);
+    RJ_HIP(hipMemcpyAsync(w->Kd, w->Kh, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice,
+                          w->s[0]));
+    return 0;
+  }
+  int64_t* idx_h(int region) { return w->idxh + region * w->cap_n; }
+  int64_t* idx_d(int region) { return w->idxd + region * w->cap_n; }
+  // the plan's chain order as a device index list (main stream)
+  int upload_order(const Plan& pl, int region) {
+    std::copy(pl.order.begin(), pl.order.end(), idx_h(region));
+    if (!pl.order.empty())
+      RJ_HIP(hipMemcpyAsync(idx_d(region), idx_h(region), pl.order.size() * sizeof(int64_t),
+                            hipMemcpyHostToDevice, w->s[0]));
+    return 0;
+  }
+  // aux waits for main, or main for aux
+  int join(int from, int to, int e) {
+    RJ_HIP(hipEventRecord(w->ev[e], w->s[from]));
+    RJ_HIP(hipStreamWaitEvent(w->s[to], w->ev[e], 0));
+    return 0;
+  }
+
+  // n_steps steps on chains idx (rows of Q, P)
+  int trajectories(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t n_steps,
+                   int region) {
+    if (idx.empty()) return 0;
+    const Plan pl = make_plan(idx, K, ragged_ok);
+    RJ_TRY(upload_order(pl, region));
+    bool aux_used = false;
+    int packed = 0;
+    for (const Call& c : pl.calls) {
+      const int64_t* rows = idx_d(region) + c.off;
+      if (c.ragged) {
+        if (int rc = rhmc_leapfrog_ragged_device(ctx, P, w->Q, w->P, W, rows, w->Kd, c.n, c.Kmin,
+                                                 c.Kmax, n_steps, w->s[0]))
+          return engine_fail(rc, "ragged steps");
+        continue;
+      }
+      // packed: gather, fixed-K steps, scatter — alternate groups onto aux
+      const int si = (packed++ % 2);
+      if (si == 1 && !aux_used) {
+        RJ_TRY(join(0, 1, 0));
+        aux_used = true;
+      }
+      hipStream_t st = w->s[si];
+      const int64_t d = 3 * (int64_t)c.Kmin;
+      double* pq = w->pack + (si ? 2 * n * W : 0);
+      double* pp = pq + c.n * d;
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, rows, pq, d, nullptr, c.n, (int32_t)d, st))
+        return engine_fail(rc, "gather");
+      if (int rc = rhmc_rows_copy_device(ctx, w->P, W, rows, pp, d, nullptr, c.n, (int32_t)d, st))
+        return engine_fail(rc, "gather");
+      if (int rc = rhmc_leapfrog_device(ctx, P, pq, pp, c.n, c.Kmin, n_steps, nullptr, nullptr, st))
+        return engine_fail(rc, "steps");
+      if (int rc = rhmc_rows_copy_device(ctx, pq, d, nullptr, w->Q, W, rows, c.n, (int32_t)d, st))
+        return engine_fail(rc, "scatter");
+      if (int rc = rhmc_rows_copy_device(ctx, pp, d, nullptr, w->P, W, rows, c.n, (int32_t)d, st))
+        return engine_fail(rc, "scatter");
+    }
+    if (aux_used) RJ_TRY(join(1, 0, 1));
+    return 0;
+  }
+
+  // V of chains idx (rows of Q) -> Vh[j] for chain order[j]; D2H on main (not synced)
+  int energies(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t f_pos,
+               std::vector<int64_t>& order, int region) {
+    order.clear();
+    if (idx.empty()) return 0;
+    const Plan pl = make_plan(idx, K, ragged_ok);
+    order = pl.order;
+    RJ_TRY(upload_order(pl, region));
+    for (const Call& c : pl.calls) {
+      const int64_t* rows = idx_d(region) + c.off;
+      if (c.ragged) {
+        if (int rc = rhmc_energy_ragged_device(ctx, P, w->Q, W, rows, w->Kd, c.n, c.Kmin, c.Kmax,
+                                               f_pos, w->V + c.off, w->s[0]))
+          return engine_fail(rc, "ragged energy");
+        continue;
+      }
+      const int64_t d = 3 * (int64_t)c.Kmin;
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, rows, w->pack, d, nullptr, c.n, (int32_t)d,
+                                         w->s[0]))
+        return engine_fail(rc, "gather");
+      if (int rc = rhmc_energy_device(ctx, P, w->pack, nullptr, w->V + c.off, nullptr, c.n, c.Kmin,
+                                      f_pos, w->s[0]))
+        return engine_fail(rc, "energy");
+    }
+    RJ_HIP(hipMemcpyAsync(w->Vh, w->V, pl.order.size() * sizeof(double), hipMemcpyDeviceToHost,
+                          w->s[0]));
+    return 0;
+  }
+};
+
+// The device-resident run of chains [0, n) of one pipe (q, K, seeds point at
+// its first chain; record row l of chain c is l * rec_stride + rec_off + c).
+int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
+               const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
+               const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
+               double* phase_out) {
+  const int64_t W = 3 * (int64_t)cfg->N_max;
+  RJ_TRY(w->ensure(dev, n, W));
+  hipStream_t s0 = w->s[0], s1 = w->s[1];
+  Run R;
+  R.phys = nullptr;
+  R.P = *P0;
+  R.cfg = cfg;
+  R.Kmax = cfg->N_max;
+  R.beta.set(cfg->beta_a, cfg->beta_b);
+  R.nt = nt;
+  Pool pool(nt);
+  R.pool = &pool;
+  R.ch.resize((size_t)n);
+  std::vector<int32_t> Kc((size_t)n);
+  std::vector<int64_t> all((size_t)n);
+  for (int64_t c = 0; c < n; ++c) {
+    all[c] = c;
+    Chain& h = R.ch[c];
+    if (cfg->use_states) {
+      const rhmc_np_state& st = cfg->states[rec_off + c];
+      h.rng.set_state(st.key, st.pos, st.has_gauss, st.gauss);
+    } else {
+      h.rng.seed(seeds[c]);
+    }
+    h.K = K[c];
+    Kc[c] = K[c];
+  }
+  // the caller's rows -> Q0 (zeros past 3 K)
+  R.parallel(all, [&](int64_t c) {
+    double* row = w->Zh + c * W;
+    std::copy(q + c * W, q + c * W + 3 * (int64_t)K[c], row);
+    std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
+  });
+  RJ_HIP(hipMemcpyAsync(w->Q0, w->Zh, (size_t)(n * W) * 8, hipMemcpyHostToDevice, s0));
+  RJ_HIP(hipStreamSynchronize(s0));  // Zh is the draws' staging next
+  std::vector<char> ragged_ok(257, 0);
+  {
+    int32_t ok = 0;
+    for (int k = 1; k <= std::min(256, cfg->N_max); ++k) {
+      if (int rc = rhmc_ragged_ok(ctx, P0, k, &ok)) return rc;
+      ragged_ok[k] = (char)ok;
+    }
+  }
+  DevRun D{ctx, w, n, W, Kc, ragged_ok};
+  const int64_t rows_n = (int64_t)cfg->n_iter + 1;
+  std::vector<double> V0((size_t)n), V1((size_t)n), V_end((size_t)n);
+  double V_end_g_ff2 = 0., V_end_beta = 0.;
+  bool V_end_ok = false;
+  const bool rec_q = rec && rec->q_chain, rec_p = rec && rec->p_chain;
+  double phase[7] = {0, 0, 0, 0, 0, 0, 0};
+  auto clk = std::chrono::steady_clock::now();
+  auto lap = [&](int i) {
+    const auto t = std::chrono::steady_clock::now();
+    phase[i] += std::chrono::duration<double>(t - clk).count();
+    clk = t;
+  };
+  std::vector<int64_t> order, jump, live, scored, acc_rows;
+  for (int64_t l = 0; l < rows_n; ++l) {
+    if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
+    if (cfg->n_beta > 0) R.P.beta = cfg->schedule_beta[std::min<int64_t>(l, cfg->n_beta - 1)];
+    const Metric M = R.metric();
+    // 1. host draws: z = randn(3K) (the momentum, :1021-1022), move type, grow / shrink
+    int64_t zt = 0;
+    for (int64_t c = 0; c < n; ++c) {
+      w->zoffh[c] = zt;
+      zt += 3 * (int64_t)Kc[c];
+    }
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      double* z = w->Zh + w->zoffh[c];
+      for (int64_t i = 0; i < 3 * (int64_t)h.K; ++i) z[i] = h.rng.gauss();
+      h.move = (int)choice(h.rng, cfg->P_move, 3, h.cdf);
+      h.grow = false;
+      if (h.move != 0) {
+        const double half[2] = {0.5, 0.5};
+        h.grow = choice(h.rng, half, 2, h.cdf) == 0;  // [True, False]
+      }
+      h.K0 = h.K;
+      h.dead = false;
+    });
+    lap(0);
+    // 2. device: Q = Q0, p = z sqrt(H(q)), T0; record rows; V(q) unless reused
+    RJ_TRY(D.upload_K());
+    RJ_HIP(hipMemcpyAsync(w->Z, w->Zh, (size_t)zt * 8, hipMemcpyHostToDevice, s0));
+    RJ_HIP(hipMemcpyAsync(w->zoffd, w->zoffh, (size_t)n * 8, hipMemcpyHostToDevice, s0));
+    RJ_HIP(hipMemcpyAsync(w->Q, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToDevice, s0));
+    if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, w->Z, w->zoffd, n,
+                                          w->T0, s0))
+      return D.engine_fail(rc, "momentum");
+    RJ_HIP(hipMemcpyAsync(w->T0h, w->T0, (size_t)n * 8, hipMemcpyDeviceToHost, s0));
+    if (rec_p)
+      RJ_HIP(hipMemcpyAsync(w->Ps, w->P, (size_t)(n * W) * 8, hipMemcpyDeviceToDevice, s0));
+    if (rec_q || rec_p) {  // the record rows leave on the aux stream
+      RJ_TRY(D.join(0, 1, 2));
+      if (rec_q)
+        RJ_HIP(hipMemcpyAsync(w->recq, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s1));
+      if (rec_p)
+        RJ_HIP(hipMemcpyAsync(w->recp, w->Ps, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s1));
+    }
+    const bool reuse = V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta;
+    if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order, kIdxV0));
+    RJ_HIP(hipEventRecord(w->ev[3], s0));  // T0h and Vh are on their way
+    // 3. the trajectory of every chain (queued behind the above)
+    RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1));
+    // the iteration's records while the GPU integrates
+    RJ_HIP(hipStreamSynchronize(s1));
+    RJ_HIP(hipEventSynchronize(w->ev[3]));
+    if (reuse) {
+      V0 = V_end;
+    } else {
+      for (size_t j = 0; j < order.size(); ++j) V0[order[j]] = w->Vh[j];
+    }
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      h.E0 = V0[c] + w->T0h[c];
+      const int64_t r = l * rec_stride + rec_off + c;
+      if (rec) {
+        if (rec_q) std::copy(w->recq + c * W, w->recq + (c + 1) * W, rec->q_chain + r * W);
+        if (rec_p) std::copy(w->recp + c * W, w->recp + (c + 1) * W, rec->p_chain + r * W);
+        if (rec->V_chain) rec->V_chain[r] = V0[c];
+        if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
+        if (rec->E_chain) rec->E_chain[r] = h.E0;
+        if (rec->n_stars) rec->n_stars[r] = h.K;
+        if (rec->move)
+          rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
+      }
+    });
+    lap(1);
+    // 4. the jumping chains' rows to the host, their proposals on (q, -p), back
+    jump.clear();
+    for (int64_t c = 0; c < n; ++c)
+      if (R.ch[c].move != 0) jump.push_back(c);
+    const int64_t nj = (int64_t)jump.size();
+    double* Jq = w->J;
+    double* Jp = w->J + n * W;
+    int64_t* jd = D.idx_d(kIdxJump);
+    if (nj > 0) {
+      std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
+      RJ_HIP(hipMemcpyAsync(jd, D.idx_h(kIdxJump), (size_t)nj * 8, hipMemcpyHostToDevice, s0));
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, W, nullptr, nj, (int32_t)W, s0))
+        return D.engine_fail(rc, "gather");
+      if (int rc = rhmc_rows_copy_device(ctx, w->P, W, jd, Jp, W, nullptr, nj, (int32_t)W, s0))
+        return D.engine_fail(rc, "gather");
+      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(nj * W) * 8, hipMemcpyDeviceToHost, s0));
+      RJ_HIP(hipMemcpyAsync(w->Jh + n * W, Jp, (size_t)(nj * W) * 8, hipMemcpyDeviceToHost, s0));
+    }
+    RJ_HIP(hipStreamSynchronize(s0));
+    lap(2);
+    std::vector<int64_t> jpos(jump.size());
+    for (int64_t j = 0; j < nj; ++j) jpos[j] = j;
+    R.parallel(jpos, [&](int64_t j) {
+      Chain& h = R.ch[jump[j]];
+      double* rq = w->Jh + j * W;
+      double* rp = w->Jh + n * W + j * W;
+      const int64_t d = 3 * (int64_t)h.K;
+      h.q.assign(rq, rq + d);
+      h.p.resize((size_t)d);
+      for (int64_t i = 0; i < d; ++i) h.p[i] = -rp[i];
+      const bool ok = h.move == 1 ? R.birth_death(h, M) : R.split_merge(h, M);
+      if (!ok) {
+        h.dead = true;
+        h.K = h.K0;
+        return;  // its rows are restored from Q0 at the accept step
+      }
+      std::fill(std::copy(h.q.begin(), h.q.end(), rq), rq + W, 0.);
+      std::fill(std::copy(h.p.begin(), h.p.end(), rp), rp + W, 0.);
+    });
+    live.clear();
+    for (int64_t c : jump)
+      if (!R.ch[c].dead) live.push_back(c);
+    for (int64_t c : live) Kc[c] = R.ch[c].K;
+    lap(3);
+    if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
+      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(nj * W) * 8, hipMemcpyHostToDevice, s0));
+      RJ_HIP(hipMemcpyAsync(Jp, w->Jh + n * W, (size_t)(nj * W) * 8, hipMemcpyHostToDevice, s0));
+      if (int rc = rhmc_rows_copy_device(ctx, Jq, W, nullptr, w->Q, W, jd, nj, (int32_t)W, s0))
+        return D.engine_fail(rc, "scatter");
+      if (int rc = rhmc_rows_copy_device(ctx, Jp, W, nullptr, w->P, W, jd, nj, (int32_t)W, s0))
+        return D.engine_fail(rc, "scatter");
+      RJ_TRY(D.upload_K());
+    }
+    // 5. the trajectory after the jump
+    RJ_TRY(D.trajectories(&R.P, live, cfg->n_steps, kIdxSteps2));
+    lap(4);
+    // 6. V(q') and T(p', H(q')) of every chain that was not a dead end
+    scored.clear();
+    for (int64_t c = 0; c < n; ++c)
+      if (!R.ch[c].dead) scored.push_back(c);
+    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1));
+    if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, nullptr, nullptr, n,
+                                          w->T1, s0))
+      return D.engine_fail(rc, "kinetic");
+    RJ_HIP(hipMemcpyAsync(w->T1h, w->T1, (size_t)n * 8, hipMemcpyDeviceToHost, s0));
+    RJ_HIP(hipStreamSynchronize(s0));
+    for (size_t j = 0; j < order.size(); ++j) V1[order[j]] = w->Vh[j];
+    lap(5);
+    // 7. accept / reject (:1072-1083, :1120-1131); accepted rows become Q0
+    std::vector<char> acc((size_t)n, 0);
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      const int64_t r = l * rec_stride + rec_off + c;
+      bool a = false;
+      if (!h.dead) {
+        const double E1 = V1[c] + w->T1h[c];
+        const double u = std::log(h.rng.random_sample());
+        if (h.move == 0) {
+          const double dE = E1 - h.E0;
+          a = (dE < 0) || (u < -dE);
+        } else {
+          const double ln_alpha0 = -(E1 - h.E0) + h.factor;
+          a = (ln_alpha0 > 0) || (u < ln_alpha0);
+        }
+        if (!a) h.K = h.K0;
+      }
+      acc[c] = a;
+      V_end[c] = a ? V1[c] : V0[c];
+      if (rec) {
+        if (rec->accept) rec->accept[r] = a ? 1 : 0;
+        if (rec->flags) rec->flags[r] = h.dead ? (int32_t)RHMC_RJ_DEAD_END : 0;
+      }
+    });
+    acc_rows.clear();
+    for (int64_t c = 0; c < n; ++c) {
+      Kc[c] = R.ch[c].K;
+      if (acc[c]) acc_rows.push_back(c);
+    }
+    if (!acc_rows.empty()) {
+      int64_t* cd = D.idx_d(kIdxCommit);
+      std::copy(acc_rows.begin(), acc_rows.end(), D.idx_h(kIdxCommit));
+      RJ_HIP(hipMemcpyAsync(cd, D.idx_h(kIdxCommit), acc_rows.size() * 8, hipMemcpyHostToDevice,
+                            s0));
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, cd, w->Q0, W, cd,
+                                         (int64_t)acc_rows.size(), (int32_t)W, s0))
+        return D.engine_fail(rc, "commit");
+    }
+    lap(6);
+    V_end_g_ff2 = R.P.g_ff2;
+    V_end_beta = R.P.beta;
+    V_end_ok = true;
+  }
+  // the final states
+  RJ_HIP(hipMemcpyAsync(w->Zh, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s0));
+  RJ_HIP(hipStreamSynchronize(s0));
+  std::copy(w->Zh, w->Zh + n * W, q);
+  for (int64_t c = 0; c < n; ++c) {
+    const Chain& h = R.ch[c];
+    K[c] = h.K;
+    if (cfg->states) {
+      rhmc_np_state& st = cfg->states[rec_off + c];
+      h.rng.get_state(st.key, &st.pos, &st.has_gauss, &st.gauss);
+    }
+  }
+  if (phase_out)
+    for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];
   return 0;
-}
-
-// One 1-chain, 0-step trajectory of the run's first star count on each stream
-// the first time the process meets that (device, kernel): the first dispatch
-// of a kernel on a hardware queue set up its scratch and cost 6-8 ms inside a
-// run (profiles/r04_rj/trace).
-std::map<std::pair<int, int>, bool> g_warm;  // (device, K) under g_streams_mu
-
-int engine_warm(CtxEngine& E, const rhmc_params* P, int32_t K) {
-  int dev = 0;
-  RJ_HIP(hipGetDevice(&dev));
-  std::lock_guard<std::mutex> lock(g_streams_mu);
-  bool& done = g_warm[{dev, K}];
-  if (done) return 0;
-  double* d = nullptr;
-  std::vector<double> h(6 * (size_t)K, 0.0);  // q: stars of 1000 counts at (1 + k/2, 2), p = 0
-  for (int32_t k = 0; k < K; ++k) {
-    h[3 * k] = 1000.0;
-    h[3 * k + 1] = 1.0 + 0.5 * k;
-    h[3 * k + 2] = 2.0;
-  }
-  RJ_HIP(hipMalloc(&d, h.size() * sizeof(double)));
-  RJ_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
-  int rc = 0;
-  for (int i = 0; i < kStreams && rc == 0; ++i)
-    rc = rhmc_leapfrog_device(E.ctx, P, d, d + 3 * K, 1, K, 0, nullptr, nullptr, E.s[i]);
-  for (int i = 0; i < kStreams; ++i) (void)hipStreamSynchronize(E.s[i]);
-  (void)hipFree(d);
-  if (rc) return rc;
-  done = true;
-  return 0;
-}
-
-int ctx_energy(void* user, const rhmc_params* P, const double* q, int64_t n, int32_t K,
-               int32_t f_pos, double* V) {
-  return rhmc_energy(static_cast<CtxEngine*>(user)->ctx, P, q, nullptr, V, nullptr, n, K, f_pos);
-}
-int ctx_steps(void* user, const rhmc_params* P, double* q, double* p, int64_t n, int32_t K,
-              int32_t n_steps) {
-  return rhmc_leapfrog(static_cast<CtxEngine*>(user)->ctx, P, q, p, n, K, n_steps, nullptr,
-                       nullptr);
-}
-double* ctx_buffer(void* user, size_t doubles) {
-  CtxEngine& E = *static_cast<CtxEngine*>(user);
-  const size_t bytes = doubles * 8;
-  if (bytes > E.d_bytes) {
-    if (E.d) (void)hipFree(E.d);
-    E.d = nullptr;
-    E.d_bytes = 0;
-    if (hipMalloc(&E.d, bytes) != hipSuccess) {
-      g_err = "hipMalloc failed";
-      return nullptr;
-    }
-    E.d_bytes = bytes;
-  }
-  if (bytes > E.h_bytes) {
-    if (E.h) (void)hipHostFree(E.h);
-    E.h = nullptr;
-    E.h_bytes = 0;
-    if (hipHostMalloc(&E.h, bytes, hipHostMallocDefault) != hipSuccess) {
-      g_err = "hipHostMalloc failed";
-      return nullptr;
-    }
-    E.h_bytes = bytes;
-  }
-  return E.h;
-}
-
-int ctx_launch(void* user, const rhmc_params* P, int32_t G, const int32_t* K, const int64_t* n,
-               const size_t* off, int32_t n_steps) {
-  CtxEngine& E = *static_cast<CtxEngine*>(user);
-  std::vector<int32_t> order((size_t)G);
-  for (int32_t g = 0; g < G; ++g) order[g] = g;
-  std::stable_sort(order.begin(), order.end(),
-                   [&](int32_t a, int32_t b) { return n[a] * K[a] > n[b] * K[b]; });
-  int rc = 0;
-  for (int32_t i = 0; i < G && rc == 0; ++i) {  // largest groups first
-    const int32_t g = order[i];
-    const size_t sb = (size_t)n[g] * 3 * (size_t)K[g];
-    hipStream_t st = E.s[i % E.ns];
-    double* hq = E.h + off[g];
-    double* dq = E.d + off[g];
-    hipError_t e = hipMemcpyAsync(dq, hq, 2 * sb * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) {
-      rc = rhmc_leapfrog_device(E.ctx, P, dq, dq + sb, n[g], K[g], n_steps, nullptr, nullptr, st);
-      if (rc == 0) e = hipMemcpyAsync(hq, dq, 2 * sb * 8, hipMemcpyDeviceToHost, st);
-    }
-    if (e != hipSuccess) rc = fail(RHMC_ERR_HIP, std::string("staging copy: ") + hipGetErrorString(e));
-  }
-  for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
-  return rc;
-}
-
-int ctx_energy_staged(void* user, const rhmc_params* P, int32_t G, const int32_t* K,
-                      const int64_t* n, const size_t* off, int32_t f_pos) {
-  CtxEngine& E = *static_cast<CtxEngine*>(user);
-  int rc = 0;
-  for (int32_t g = 0; g < G && rc == 0; ++g) {
-    const size_t sb = (size_t)n[g] * 3 * (size_t)K[g];
-    hipStream_t st = E.s[g % E.ns];
-    double* hq = E.h + off[g];
-    double* dq = E.d + off[g];
-    hipError_t e = hipMemcpyAsync(dq, hq, sb * 8, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) {
-      rc = rhmc_energy_device(E.ctx, P, dq, nullptr, dq + sb, nullptr, n[g], K[g], f_pos, st);
-      if (rc == 0) e = hipMemcpyAsync(hq + sb, dq + sb, (size_t)n[g] * 8, hipMemcpyDeviceToHost, st);
-    }
-    if (e != hipSuccess) rc = fail(RHMC_ERR_HIP, std::string("staging copy: ") + hipGetErrorString(e));
-  }
-  for (int i = 0; i < E.ns; ++i) RJ_HIP(hipStreamSynchronize(E.s[i]));
-  return rc;
 }
 
 // Split n chains into `pipes` contiguous parts run concurrently, part i on
@@ -1029,7 +1302,7 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
     const int64_t W = 3 * (int64_t)cfg->N_max;
     int rc = run_pipes(cfg->n_pipes > 1 ? pipes_for(cfg, n) : 1, n, nt, phase,
                        [&](int, int64_t f, int64_t m, int t, double* ph) {
-                         return run(phys, nullptr, P, cfg, q + f * W, K + f,
+                         return run(phys, P, cfg, q + f * W, K + f,
                                     seeds ? seeds + f : nullptr, m, rec, n, f, t, ph);
                        });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
@@ -1044,35 +1317,30 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   try {
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
-    CtxEngine E[kMaxPipes];
-    for (auto& e : E) e.ctx = ctx;
-    if (int rc = engine_init(E[0])) return rc;
-    if (n > 0)
-      if (int rc = engine_warm(E[0], P, K[0])) return rc;
+    const double* dimg = nullptr;
+    if (int rc = rhmc_ctx_image_device(ctx, &dimg)) return rc;
+    if (!dimg) return fail(RHMC_ERR_ARG, "context has no image");
+    hipPointerAttribute_t at;
+    RJ_HIP(hipPointerGetAttributes(&at, dimg));
+    const int dev = at.device;
+    DeviceGuard guard;  // the caller's device comes back on return
+    RJ_HIP(hipSetDevice(dev));
     const int pipes = pipes_for(cfg, n);
     const int nt = host_threads(cfg);
-    // pipe i takes streams i, i + pipes, ... (the HIP calls of the *_device
-    // entry points touch no shared context state)
-    hipStream_t all_s[kStreams];
-    std::copy(E[0].s, E[0].s + kStreams, all_s);
+    // each pipe on its own process-lifetime buffers and streams, held for the run
+    Work* works[kMaxPipes] = {};
+    std::unique_lock<std::mutex> locks[kMaxPipes];
     for (int i = 0; i < pipes; ++i) {
-      E[i].dev = E[0].dev;
-      E[i].ns = 0;
-      for (int j = i; j < kStreams; j += pipes) E[i].s[E[i].ns++] = all_s[j];
+      works[i] = work_for(dev, i);
+      locks[i] = std::unique_lock<std::mutex>(works[i]->mu);
     }
     const int64_t W = 3 * (int64_t)cfg->N_max;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};
     const int rc = run_pipes(pipes, n, nt, phase, [&](int i, int64_t f, int64_t m, int t,
                                                       double* ph) {
-      if (i > 0 && hipSetDevice(E[i].dev) != hipSuccess) return fail(RHMC_ERR_HIP, "hipSetDevice failed");
-      rhmc_rj_physics phys{&E[i], ctx_energy, ctx_steps};
-      Run::Staged st;
-      st.user = &E[i];
-      st.buffer = ctx_buffer;
-      st.launch = ctx_launch;
-      st.energy = ctx_energy_staged;
-      return run(&phys, &st, P, cfg, q + f * W, K + f, seeds ? seeds + f : nullptr, m, rec, n, f,
-                 t, ph);
+      if (hipSetDevice(dev) != hipSuccess) return fail(RHMC_ERR_HIP, "hipSetDevice failed");
+      return run_device(ctx, dev, works[i], P, cfg, q + f * W, K + f, seeds ? seeds + f : nullptr,
+                        m, rec, n, f, t, ph);
     });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
@@ -1097,6 +1365,29 @@ int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, do
       case 5: out[i] = r.standard_exponential(); break;
       default: return fail(RHMC_ERR_ARG, "unknown kind");
     }
+  }
+  return 0;
+}
+
+int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
+                        double flux_to_count, double* q) {
+  if (n < 0 || N_max < 1) return fail(RHMC_ERR_ARG, "bad n or N_max");
+  if (n > 0 && (!rows || !K || !q)) return fail(RHMC_ERR_ARG, "rows, K or q is NULL");
+  const int64_t W = 3 * (int64_t)N_max;
+  int64_t at = 0;
+  for (int64_t c = 0; c < n; ++c)
+    if (K[c] < 1 || K[c] > N_max) return fail(RHMC_ERR_ARG, "K[c] must be in [1, N_max]");
+  for (int64_t c = 0; c < n; ++c) {
+    double* row = q + c * W;
+    for (int32_t k = 0; k < K[c]; ++k, at += 3) {
+      const double v = rows[at];
+      // mag2flux_converter (sampler_RHMC.py:147-152, utils.py:24-25): libm pow,
+      // the function NumPy's and Python's float power call
+      row[3 * k] = flux_to_count > 0 ? std::pow(10.0, 0.4 * (22.5 - v)) * flux_to_count : v;
+      row[3 * k + 1] = rows[at + 1];
+      row[3 * k + 2] = rows[at + 2];
+    }
+    std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
   }
   return 0;
 }

@@ -49,8 +49,10 @@ EXPORTS = ("rhmc_abi_version", "rhmc_device_count", "rhmc_last_error",
            "rhmc_mh",
            "rhmc_mh_device", "rhmc_integrate", "rhmc_integrate_device",
            "rhmc_gen_image", "rhmc_gen_image_device", "rhmc_hmc_random",
-           "rhmc_hmc_random_device", "rhmc_mh_scheduled", "rhmc_mh_scheduled_device")
-ABI_VERSION = 3
+           "rhmc_hmc_random_device", "rhmc_mh_scheduled", "rhmc_mh_scheduled_device",
+           "rhmc_ragged_ok", "rhmc_leapfrog_ragged_device", "rhmc_energy_ragged_device",
+           "rhmc_rows_copy_device", "rhmc_kinetic_rows_device")
+ABI_VERSION = 4
 
 V_FLUX_WALL = 1       # rhmc_energy f_pos bits (include/rhmc.h)
 V_NO_POSCHECK = 2
@@ -173,6 +175,17 @@ def _load():
         "rhmc_gen_image_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int32,
                                                  ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
                                                  ctypes.c_uint64, vp, vp]),
+        "rhmc_ragged_ok": (ctypes.c_int, [vp, P(RhmcParams), ctypes.c_int32, P(ctypes.c_int32)]),
+        "rhmc_leapfrog_ragged_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, ctypes.c_int64,
+                                                       vp, vp, ctypes.c_int64, ctypes.c_int32,
+                                                       ctypes.c_int32, ctypes.c_int32, vp]),
+        "rhmc_energy_ragged_device": (ctypes.c_int, [vp, P(RhmcParams), vp, ctypes.c_int64, vp,
+                                                     vp, ctypes.c_int64, ctypes.c_int32,
+                                                     ctypes.c_int32, ctypes.c_int32, vp, vp]),
+        "rhmc_rows_copy_device": (ctypes.c_int, [vp, vp, ctypes.c_int64, vp, vp, ctypes.c_int64,
+                                                 vp, ctypes.c_int64, ctypes.c_int32, vp]),
+        "rhmc_kinetic_rows_device": (ctypes.c_int, [vp, P(RhmcParams), vp, vp, ctypes.c_int64,
+                                                    vp, vp, vp, ctypes.c_int64, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -339,6 +352,42 @@ class Context:
                                        ctypes.c_void_p(p_ptr or 0), ctypes.c_void_p(V_ptr or 0),
                                        ctypes.c_void_p(T_ptr or 0), int(n_chains), int(K),
                                        int(f_pos), ctypes.c_void_p(stream or 0)))
+
+    # ---- ragged chain sets (ABI 4; device pointers, asynchronous on `stream`)
+    def ragged_ok(self, params, K):
+        """Whether chains of K stars can share ragged launches on this image."""
+        ok = ctypes.c_int32(0)
+        _check(_lib.rhmc_ragged_ok(self._h, ctypes.byref(params), int(K), ctypes.byref(ok)))
+        return bool(ok.value)
+
+    def leapfrog_ragged_device(self, params, q_ptr, p_ptr, ld, rows_ptr, K_ptr, n, K_min, K_max,
+                               n_steps, stream=None):
+        _check(_lib.rhmc_leapfrog_ragged_device(
+            self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr), ctypes.c_void_p(p_ptr),
+            int(ld), ctypes.c_void_p(rows_ptr or 0), ctypes.c_void_p(K_ptr), int(n), int(K_min),
+            int(K_max), int(n_steps), ctypes.c_void_p(stream or 0)))
+
+    def energy_ragged_device(self, params, q_ptr, ld, rows_ptr, K_ptr, n, K_min, K_max, f_pos,
+                             V_ptr, stream=None):
+        _check(_lib.rhmc_energy_ragged_device(
+            self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr), int(ld),
+            ctypes.c_void_p(rows_ptr or 0), ctypes.c_void_p(K_ptr), int(n), int(K_min),
+            int(K_max), int(f_pos), ctypes.c_void_p(V_ptr), ctypes.c_void_p(stream or 0)))
+
+    def rows_copy_device(self, src_ptr, ld_src, src_rows_ptr, dst_ptr, ld_dst, dst_rows_ptr, n,
+                         width, stream=None):
+        _check(_lib.rhmc_rows_copy_device(
+            self._h, ctypes.c_void_p(src_ptr), int(ld_src), ctypes.c_void_p(src_rows_ptr or 0),
+            ctypes.c_void_p(dst_ptr), int(ld_dst), ctypes.c_void_p(dst_rows_ptr or 0), int(n),
+            int(width), ctypes.c_void_p(stream or 0)))
+
+    def kinetic_rows_device(self, params, q_ptr, p_ptr, ld, K_ptr, z_ptr, zoff_ptr, n, T_ptr,
+                            stream=None):
+        _check(_lib.rhmc_kinetic_rows_device(
+            self._h, ctypes.byref(params), ctypes.c_void_p(q_ptr), ctypes.c_void_p(p_ptr),
+            int(ld), ctypes.c_void_p(K_ptr), ctypes.c_void_p(z_ptr or 0),
+            ctypes.c_void_p(zoff_ptr or 0), int(n), ctypes.c_void_p(T_ptr),
+            ctypes.c_void_p(stream or 0)))
 
     def gradient(self, params, q, kind=0):
         q2 = np.array(q, dtype=np.float64, order="C", copy=True)

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so")
 DEAD_END = 1                 # RHMC_RJ_DEAD_END
 
 EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_beta_eval",
-           "rhmc_rj_last_error")
+           "rhmc_rj_pack_starts", "rhmc_rj_last_error")
 
 ENERGY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
                              ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int32,
@@ -91,6 +91,7 @@ def _load():
         "rhmc_np_draws": [ctypes.c_uint32, ctypes.c_int32, ctypes.c_double, ctypes.c_double,
                           ctypes.c_int64, vp],
         "rhmc_rj_beta_eval": [ctypes.c_double, ctypes.c_double, vp, ctypes.c_int64, vp, vp],
+        "rhmc_rj_pack_starts": [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, vp],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -135,28 +136,46 @@ def beta_eval(a, b, x):
     return pdf, logpdf
 
 
+def pack_starts(q_models, N_max, flux_to_count=0.):
+    """Chain starts -> (q [n][3 N_max] zero-padded, K [n]) in one native pass.
+    q_models: [K_c, 3] arrays — (mag, x, y) rows converted by format_q's
+    mag2flux (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 —
+    or flat flux-count vectors with flux_to_count = 0."""
+    n = len(q_models)
+    K = np.fromiter((np.size(m) // 3 for m in q_models), dtype=np.int32, count=n)
+    if n and (K.min() < 1 or K.max() > N_max or
+              any(np.size(m) % 3 for m in q_models)):
+        raise ValueError("every start needs 1 .. N_max stars (3 values each)")
+    rows = np.ascontiguousarray(np.concatenate([np.ravel(m) for m in q_models])
+                                if n else np.zeros(0), dtype=np.float64)
+    q = np.empty((n, 3 * int(N_max)))
+    _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
+                                    float(flux_to_count), q.ctypes.data))
+    return q, K
+
+
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0, n_pipes=0, states=None):
+        n_threads=0, n_pipes=0, states=None, packed=None):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
-    vectors.  Either ctx (a capi.Context: the engine) or physics (a pair of
+    vectors, or None with packed = (q [n][3 N_max], K [n]) from pack_starts.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
     -> None, in place; for stand-ins).  states: None (streams from the seeds)
     or an array of STATE_DTYPE rows to start from (then seeds may be None).
     Returns (q list, record dict); record["states"] holds every chain's stream
     at the end (pass it back as `states` to resume)."""
-    n = len(q_models)
+    W = 3 * int(N_max)
+    if packed is not None:
+        q, K = packed
+        q = np.ascontiguousarray(q, dtype=np.float64)
+        K = np.ascontiguousarray(K, dtype=np.int32)
+        if q.shape != (K.size, W):
+            raise ValueError("packed q must be [n][3 N_max]")
+    else:
+        q, K = pack_starts(q_models, N_max)
+    n = K.size
     if states is None and (seeds is None or len(seeds) != n):
         raise ValueError("one seed per chain")
-    W = 3 * int(N_max)
-    q = np.zeros((n, W))
-    K = np.empty(n, dtype=np.int32)
-    for c, qm in enumerate(q_models):
-        qm = np.asarray(qm, dtype=np.float64).ravel()
-        if qm.size % 3 or qm.size // 3 > N_max:
-            raise ValueError("chain %d: %d values for N_max %d" % (c, qm.size, N_max))
-        q[c, :qm.size] = qm
-        K[c] = qm.size // 3
     if states is not None:
         st = np.ascontiguousarray(np.array(states, dtype=STATE_DTYPE))
         if st.shape != (n,):
@@ -225,4 +244,5 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
         if err:
             raise err[0]
         _check(rc)
-    return [q[c, :3 * K[c]].copy() for c in range(n)], rec
+    flat = q[np.arange(W)[None, :] < 3 * K[:, None]]     # the chains' final q, row after row
+    return np.split(flat, np.cumsum(3 * K.astype(np.int64))[:-1]) if n else [], rec

@@ -858,18 +858,26 @@ class multi_gym(base_class):
         jumps = P_move[1] != 0 or P_move[2] != 0
         if jumps and (self.alpha is None or self.fmin is None or self.fmax is None):
             assert False                                  # :1205-1207 (prior required)
-        q0 = [self._start_q(m) for m in q_models_0]
+        # the starts in one native pass: [K, 3] (mag, x, y) rows through format_q's
+        # mag2flux (bit-identical to _start_q), flat q vectors (a resume) as they are
+        dims = {np.ndim(m) for m in q_models_0}
+        if dims <= {2}:
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count)
+        elif dims <= {1}:
+            packed = rj_native.pack_starts(q_models_0, N_max)
+        else:
+            packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max)
         P = self._params(delta, counter_max, for_energy=True)
         import time
         t0 = time.perf_counter()
         q_end, rec = rj_native.run(
-            P, q0, seeds, Niter, Nsteps, N_max, P_move, capi.V_FLUX_WALL if f_pos else 0,
+            P, None, seeds, Niter, Nsteps, N_max, P_move, capi.V_FLUX_WALL if f_pos else 0,
             self.num_rows, self.num_cols, self.fmin if jumps else 1., self.fmax if jumps else 1.,
             self.K_split, self.beta_a, self.beta_b, schedule_g_ff2=schedule_g_ff2,
             schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads,
             n_pipes=n_pipes, states=(None if rng_states is None else
                                      rng_states if isinstance(rng_states, np.ndarray)
-                                     else rj_native.states_from(rng_states)))
+                                     else rj_native.states_from(rng_states)), packed=packed)
         self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
         for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):

@@ -39,6 +39,13 @@
  *       base_class.gen_model (sampler_RHMC.py:101-116), gen_mock_data
  *       (:77-99, Poisson draw utils.py:488-496) and the N_trial realisations
  *       of gen_noise_profile (:118-144), on the device.
+ *   rhmc_leapfrog_ragged_device / rhmc_energy_ragged_device /
+ *   rhmc_rows_copy_device / rhmc_kinetic_rows_device (ABI 4)
+ *       the same step and V for chains of DIFFERENT star counts in one launch,
+ *       and the momentum draw / T of run_RHMC (:1021-1026, :353-363) on
+ *       device-resident ragged sets: the reversible-jump iterations of
+ *       run_RHMC (:1018-1187), whose chains change K by births, deaths,
+ *       splits and merges (librhmc_rj.so keeps them in HBM between phases).
  *   rhmc_params
  *       the instance attributes the step reads: dt, g_xx,
  *       g_ff, g_ff2, g0, g1, g2, B_count, f_lim, mB (-> f_low),
@@ -69,7 +76,7 @@
 extern "C" {
 #endif
 
-#define RHMC_ABI_VERSION 3
+#define RHMC_ABI_VERSION 4
 
 enum {
   RHMC_OK = 0,
@@ -215,6 +222,45 @@ int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
                          double* d_p, int64_t n_chains, int32_t K,
                          int32_t n_steps, int32_t* d_fp_iters,
                          int32_t* d_status, void* stream);
+
+/*
+ * Ragged chain sets (ABI 4).  Chain i of a call is row rows[i] (d_rows NULL:
+ * row i) of padded device arrays [*][ld]; the row holds the chain's d_K[row]
+ * stars (its first 3 K entries; d_K indexed by row).  One launch serves every
+ * star count in [K_min, K_max] when the automatic dispatch runs a slotted
+ * one-wave-per-chain kernel for each of them — the dense kernel on 32/48-px
+ * images from 11 stars, the windowed kernel (rhmc_ragged_ok says which K);
+ * K_min and K_max must need the same register slots (1-64, 65-128, 129-256
+ * stars), else RHMC_ERR_ARG, and a K the slotted kernels do not serve gives
+ * RHMC_ERR_UNSUPPORTED.  Each chain's results equal those of a fixed-K call
+ * on it (the kernels are batch-invariant).  Asynchronous on `stream`.
+ */
+int rhmc_ragged_ok(rhmc_ctx* ctx, const rhmc_params* P, int32_t K, int32_t* ok);
+/* n_steps RHMC_single_step()s on the set; q, p rows updated in place. */
+int rhmc_leapfrog_ragged_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_p,
+                                int64_t ld, const int64_t* d_rows, const int32_t* d_K,
+                                int64_t n, int32_t K_min, int32_t K_max, int32_t n_steps,
+                                void* stream);
+/* V (rhmc_energy's, f_pos bits likewise) of the set: d_V[i] for chain i. */
+int rhmc_energy_ragged_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, int64_t ld,
+                              const int64_t* d_rows, const int32_t* d_K, int64_t n,
+                              int32_t K_min, int32_t K_max, int32_t f_pos, double* d_V,
+                              void* stream);
+/* dst[dst_rows[i]][0:width] = src[src_rows[i]][0:width] for i < n (either
+ * index array NULL: row i): gathers of a ragged set into packed [n][3K]
+ * batches for the fixed-K entry points, scatters back, row restores. */
+int rhmc_rows_copy_device(rhmc_ctx* ctx, const double* d_src, int64_t ld_src,
+                          const int64_t* d_src_rows, double* d_dst, int64_t ld_dst,
+                          const int64_t* d_dst_rows, int64_t n, int32_t width, void* stream);
+/* Rows 0..n-1 of a ragged set (d_K[c] stars): with d_z non-NULL first the
+ * momentum draw p = z sqrt(H(q)) (:1021-1022; chain c's 3 K normals at
+ * d_z + d_zoff[c], p zeroed past 3 K), then T[c] = (sum p^2/H(q) + sum
+ * ln|H(q)|) / 2 (:353-363) with NumPy's pairwise summation order.  H
+ * follows the reference's operation order (:260-292, g_ff2 / g_xx / B /
+ * f_low from P). */
+int rhmc_kinetic_rows_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, double* d_p,
+                             int64_t ld, const int32_t* d_K, const double* d_z,
+                             const int64_t* d_zoff, int64_t n, double* d_T, void* stream);
 
 /* kind: 0 = dVdq (:365-425), 1 = dphidq (:448-465).  Host pointers. */
 int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q,

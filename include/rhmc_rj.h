@@ -145,6 +145,14 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
  * 5: standard_exponential(). */
 int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, double* out);
 
+/* The chains' starting rows for rhmc_rj_run: rows [sum K][3] (chain after
+ * chain, K[c] rows each) -> q [n][3 N_max] zero-padded.  flux_to_count > 0:
+ * the rows are (mag, x, y) and the flux becomes mag2flux(mag) * flux_to_count
+ * (format_q, sampler_RHMC.py:209-217, with the libm pow the reference's
+ * NumPy scalars use: bit-identical); 0: the rows are already counts. */
+int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
+                        double flux_to_count, double* q);
+
 /* The split / merge moves' Beta(beta_a, beta_b) density as the driver
  * evaluates it (scipy.stats.beta.logpdf / pdf at sampler_RHMC.py:1342, :1363,
  * :1438), for parity checks: n points x -> pdf[n], logpdf[n] (each nullable).

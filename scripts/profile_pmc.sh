@@ -7,7 +7,10 @@ TAG=$(echo "$WL" | tr 'A-Z' 'a-z')
 OUT=gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-BENCH="python3 bench.py --workload $WL --steps 3 --warmup 1 --no-cpu --no-e2e"
+BENCH="python3 bench.py --workload $WL --steps 3 --warmup 1 --no-cpu --no-e2e ${PMC_ARGS:-}"
+TAG=${PMC_TAG:-$TAG}
+OUT=gpurun_out/pmc_$TAG
+mkdir -p "$OUT"
 pass() {
   local name=$1; shift
   echo "=== pmc pass $name: $*"

@@ -9,6 +9,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <new>
+#include <thread>
 #include <vector>
 
 #include "rhmc_rj.h"
@@ -43,6 +45,15 @@ static int fake_steps(void*, const rhmc_params*, double* q, double* p, int64_t n
 }
 static int bad_steps(void*, const rhmc_params*, double*, double*, int64_t, int32_t, int32_t) {
   return RHMC_ERR_HIP;
+}
+// a stand-in engine that throws (an allocation failure inside a callback) on
+// every thread but the caller's: with n_pipes > 1 the pipe threads' exceptions
+// must come back as RHMC_ERR_NOMEM, not terminate the process
+static std::thread::id g_main_thread;
+static int throwing_steps(void* u, const rhmc_params* P, double* q, double* p, int64_t n,
+                          int32_t K, int32_t n_steps) {
+  if (std::this_thread::get_id() != g_main_thread) throw std::bad_alloc();
+  return fake_steps(u, P, q, p, n, K, n_steps);
 }
 
 static rhmc_params params() {
@@ -100,29 +111,31 @@ struct Rec {
   }
 };
 
-// gpu mode: rhmc_rj_run on a real context (the staged, stream-concurrent
-// engine path, one, two and four pipes) on a synthetic 32x32 image
+// gpu mode: rhmc_rj_run on a real context (the device-resident driver: ragged
+// and packed launches, one, two and four pipes) on a synthetic 32x32 image
 static void gpu_mode(const rhmc_params& P) {
   std::vector<double> D(32 * 32);
   for (int i = 0; i < 32 * 32; ++i) D[i] = 25. + (i % 7);
   rhmc_ctx* ctx = nullptr;
   CHECK(rhmc_ctx_create(0, D.data(), 32, 32, &ctx) == 0, "ctx create");
   if (!ctx) return;
-  const int n = 45;
+  const int n = 90;
   for (int pipes = 1; pipes <= 4; pipes *= 2) {
-    rhmc_rj_config c = config(6, 16, 0.4, 0.3, 0.3);
+    rhmc_rj_config c = config(6, 90, 0.4, 0.3, 0.3);
     c.n_pipes = pipes;
     const int W = 3 * c.N_max;
     std::vector<double> q((size_t)n * W, 0.);
     std::vector<int32_t> K(n);
     std::vector<uint32_t> seeds(n);
     for (int i = 0; i < n; ++i) {
-      K[i] = 1 + i % 13;                 // one-star, pixel-major and dense kernels
+      // one-star, pixel-major (packed launches) and dense kernels (ragged
+      // launches of one and two register slots)
+      K[i] = i < 45 ? 1 + i % 13 : 11 + (i * 7) % 75;
       seeds[i] = 300u + (uint32_t)i;
       for (int k = 0; k < K[i]; ++k) {
-        q[(size_t)i * W + 3 * k] = 800. + 200. * k;
-        q[(size_t)i * W + 3 * k + 1] = 4. + 2. * k;
-        q[(size_t)i * W + 3 * k + 2] = 27. - 2. * k;
+        q[(size_t)i * W + 3 * k] = 800. + 200. * (k % 13);
+        q[(size_t)i * W + 3 * k + 1] = 4. + 2. * (k % 13);
+        q[(size_t)i * W + 3 * k + 2] = 27. - 2. * (k % 11);
       }
     }
     Rec R(c.n_iter + 1, n, W);
@@ -256,6 +269,35 @@ int main(int argc, char** argv) {
           "engine failure");
     CHECK(rhmc_rj_run(nullptr, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG, "null ctx");
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 0, nullptr) == 0, "n = 0");
+  }
+  // exceptions on pipe threads (no C++ exception may cross the ABI
+  // or leave a std::thread)
+  {
+    g_main_thread = std::this_thread::get_id();
+    rhmc_rj_physics thrower{nullptr, fake_energy, throwing_steps};
+    const int m = 40;
+    rhmc_rj_config c = config(4, 6, 0.4, 0.3, 0.3);
+    c.n_pipes = 2;
+    const int W = 3 * c.N_max;
+    std::vector<double> q((size_t)m * W, 0.);
+    std::vector<int32_t> K(m, 2);
+    std::vector<uint32_t> seeds(m);
+    for (int i = 0; i < m; ++i) {
+      seeds[i] = 500u + (uint32_t)i;
+      for (int k = 0; k < 2; ++k) {
+        q[(size_t)i * W + 3 * k] = 700. + 100. * k;
+        q[(size_t)i * W + 3 * k + 1] = 8. + 5. * k;
+        q[(size_t)i * W + 3 * k + 2] = 9. + 4. * k;
+      }
+    }
+    const int rc = rhmc_rj_run_physics(&thrower, &P, &c, q.data(), K.data(), seeds.data(), m,
+                                       nullptr);
+    CHECK(rc == RHMC_ERR_NOMEM, "exception on a pipe thread");
+    CHECK(std::strstr(rhmc_rj_last_error(), "host exception") != nullptr, "exception message");
+    c.n_pipes = 1;  // one pipe: the caller's thread, the stand-in does not throw
+    CHECK(rhmc_rj_run_physics(&thrower, &P, &c, q.data(), K.data(), seeds.data(), m, nullptr) ==
+              0,
+          "no exception on the caller's thread");
   }
   // the stream replica
   std::vector<double> d(1000);

@@ -23,7 +23,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_params_layout():
     from rhmc_amd import capi
-    assert capi.abi_version() == capi.ABI_VERSION == 3
+    assert capi.abi_version() == capi.ABI_VERSION == 4
     # 16 doubles + 4 int32 = 144 bytes, no padding
     assert ctypes.sizeof(capi.RhmcParams) == 16 * 8 + 4 * 4
     assert ctypes.sizeof(capi.MhSchedule) == 2 * 8 + 2 * 4

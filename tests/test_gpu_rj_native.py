@@ -137,6 +137,35 @@ def test_native_two_pipes_equal_one(gpu_lib):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
 
 
+def test_native_recorded_V_dense_ragged(gpu_lib):
+    """The same V-reuse check where the driver's phases are ragged dense
+    launches (32x32, 12 - 40 stars, births and splits past the starting
+    counts): every recorded V equals the engine's V of that row's q alone."""
+    zb = load_golden("traj_bigk")
+    par = R.params_from_npz(zb)
+    g = _gym(par)
+    g.D = zb["D"]
+    g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
+    rs = np.random.RandomState(31)
+    q0 = zb["Q"][0, 0].reshape(-1, 3)
+    starts = []
+    for c in range(40):
+        m = q0[rs.permutation(100)[:12 + c % 29]].copy()
+        m[:, 0] = g.flux2mag_converter(np.maximum(m[:, 0], 1.5 * par["f_lim"]))
+        starts.append(m)
+    kw = dict(f_pos=True, delta=1e-6, Niter=6, Nsteps=3, dt=0.05, N_max=48,
+              P_move=[0.4, 0.3, 0.3])
+    g.run_RHMC_rj_batched(starts, list(range(40)), **kw)
+    ctx = g._context()
+    P = g._params(kw["delta"], 1000, for_energy=True)
+    for l in range(kw["Niter"] + 1):
+        for c in range(40):
+            K = int(g.N_chain[l, c])
+            V, _ = ctx.energy(P, g.q_chain[l, c, :3 * K], f_pos=True)
+            assert V == g.V_chain[l, c] or (np.isnan(V) and np.isnan(g.V_chain[l, c])), (l, c, K)
+    assert len(np.unique(g.N_chain)) > 20 and (g.A_chain & (g.move_chain > 0)).any()
+
+
 @pytest.mark.parametrize("sched", [False, True])
 def test_native_recorded_V_is_the_engine_V_of_each_start(gpu_lib, sched):
     """The driver takes an iteration's V(q) from the previous iteration's end

@@ -36,7 +36,7 @@ def _tree(tmp_path):
 
 def test_fresh_summary_gives_a_fraction(tmp_path):
     root = _tree(tmp_path)
-    pmc, stale = bench.load_pmc("C2", root)
+    pmc, stale = bench.load_pmc("C2", root=root)
     assert not stale
     r = bench.roofline(pmc, _WL, 2048000, 1.0, stale)
     assert r["frac"] is not None and not r["pmc_stale"]
@@ -49,7 +49,7 @@ def test_one_flipped_byte_makes_it_stale(tmp_path):
     b = bytearray(open(src, "rb").read())
     b[len(b) // 2] ^= 1
     open(src, "wb").write(bytes(b))
-    pmc, stale = bench.load_pmc("C2", root)
+    pmc, stale = bench.load_pmc("C2", root=root)
     assert stale
     r = bench.roofline(pmc, _WL, 2048000, 1.0, stale)
     assert r["frac"] is None and r["achieved"] is None and r["traffic"] is None
@@ -62,4 +62,4 @@ def test_summary_without_hash_is_stale(tmp_path):
     pmc = json.load(open(path))
     del pmc["src_hash"]
     json.dump(pmc, open(path, "w"))
-    assert bench.load_pmc("C2", root)[1]
+    assert bench.load_pmc("C2", root=root)[1]

@@ -148,3 +148,25 @@ def test_format_q_fast_is_bit_identical():
     for K in (1, 3, 51, 120):
         m = np.column_stack([rs.uniform(14, 24, K), rs.uniform(0, 48, K), rs.uniform(0, 48, K)])
         assert np.array_equal(g._format_q_fast(m), g.format_q(m.copy()))
+
+
+def test_native_start_packing_is_format_q():
+    """The native RJ driver's starts (rj_native.pack_starts: one pass in C++
+    with libm pow) equal format_q of every chain (sampler_RHMC.py:209-217)
+    bit for bit, zero-padded to 3 N_max; flat flux-count starts pass
+    unchanged."""
+    from rhmc_amd import rj_native, sampler
+    g = sampler.multi_gym(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
+    rs = np.random.RandomState(12)
+    starts = [np.column_stack([15 + 8.3 * rs.rand(k), 32 * rs.rand(k), 32 * rs.rand(k)])
+              for k in (1, 5, 51, 3, 120)]
+    q, K = rj_native.pack_starts(starts, 120, g.flux_to_count)
+    assert list(K) == [1, 5, 51, 3, 120]
+    for c, m in enumerate(starts):
+        want = g.format_q(m.copy())
+        assert np.array_equal(q[c, :want.size], want)
+        assert not q[c, want.size:].any()
+    q2, K2 = rj_native.pack_starts([q[c, :3 * K[c]] for c in range(5)], 120)
+    assert np.array_equal(q2, q) and np.array_equal(K2, K)
+    with pytest.raises(ValueError):
+        rj_native.pack_starts([np.ones((2, 3))], 1)
