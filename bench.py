@@ -355,13 +355,14 @@ def bench_rj(args, wl, gpu, world, rank):
     g.device = gpu
     seeds = [1000 * rank + c for c in range(n_chains)]
     for _ in range(args.warmup):
-        g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, **kw)
+        g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, n_pipes=args.rj_pipes, **kw)
     if world > 1:
         dist.barrier()
     steps = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
-        g.run_RHMC_rj_batched([m.copy() for m in starts], [s + 7 * (i + 1) for s in seeds], **kw)
+        g.run_RHMC_rj_batched([m.copy() for m in starts], [s + 7 * (i + 1) for s in seeds],
+                              n_pipes=args.rj_pipes, **kw)
         # move 0: one trajectory; a jump: two, unless its proposal was a dead end
         steps += int(np.sum(np.where((g.move_chain == 0) | (g.flag_chain != 0), 1, 2))) * leap
     wall = time.perf_counter() - t0
@@ -380,7 +381,8 @@ def bench_rj(args, wl, gpu, world, rank):
                                "steps per run, P_move %s, N_max %d, beta_a = beta_b = %g"
                                % (name, D.shape[0], D.shape[1], K0, n_chains, n_it, leap,
                                   kw["P_move"], kw["N_max"], g.beta_a),
-                   "mode": "rj", "parallelism": "chain-sharded x%d" % world},
+                   "mode": "rj", "rj_pipes": args.rj_pipes or "auto",
+                   "parallelism": "chain-sharded x%d" % world},
         "roofline": None,
         "rj": {"accept_rate_jumps": float(np.mean(g.A_chain[g.move_chain > 0]))
                if (g.move_chain > 0).any() else None,
@@ -426,9 +428,14 @@ def main():
                          "rj: the reversible-jump run_RHMC through librhmc_rj.so, one step "
                          "= --mh-iter iterations of --leap steps (default workload: use B4)")
     ap.add_argument("--mh-iter", type=int, default=10)
+    ap.add_argument("--rj-pipes", type=int, choices=(0, 1, 2, 3, 4), default=0,
+                    help="--mode rj: host pipes of the native driver (0: its default)")
     ap.add_argument("--f-pos", type=int, choices=(0, 1), default=1,
                     help="--mode mh: run_RHMC's f_pos (V = inf below the flux wall, "
                          "sampler_RHMC.py:303-309; the reference's default 1)")
+    ap.add_argument("--mh-floor", type=float, default=1.5,
+                    help="--mode mh with --f-pos 1: chain fluxes start >= this x f_lim "
+                         "(workloads.mh_start)")
     ap.add_argument("--mh-unfused", action="store_true",
                     help="--mode mh: the four-kernel loop (RHMC_OPT_MH_FUSED = 0)")
     ap.add_argument("--window-split", type=int, choices=(0, 1, 2, 4), default=0,
@@ -532,7 +539,7 @@ def main():
         if args.f_pos:
             # with f_pos a start below the flux wall has V = inf: every proposal
             # would be rejected before any pixel work (workloads.mh_start)
-            q.copy_(torch.from_numpy(workloads.mh_start(wl)).to(dev))
+            q.copy_(torch.from_numpy(workloads.mh_start(wl, args.mh_floor)).to(dev))
         # the accept decisions of each launch (n_iter x n_chains int32 on the device)
         mh_acc = torch.zeros((args.mh_iter, wl.n_chains), dtype=torch.int32, device=dev)
         mh_rec = capi.MhRecord(None, None, None, None, mh_acc.data_ptr())
@@ -640,6 +647,8 @@ def main():
                    "leapfrog_steps_per_launch": steps_per_launch, "mode": args.mode,
                    "mh_fused": (None if args.mode != "mh" else not args.mh_unfused),
                    "f_pos": (None if args.mode != "mh" else args.f_pos),
+                   "mh_start_flux_floor": (args.mh_floor if args.mode == "mh" and args.f_pos
+                                           else None),
                    "solver": (args.solver if args.mode == "integrate" else
                               "hmc_random" if args.mode == "hmc_random" else "implicit"),
                    "parallelism": "chain-sharded x%d" % world},

@@ -20,8 +20,10 @@ MH starts (`mh_start`): the multi-star workloads draw magnitudes down to
 23.3, below the flux wall at mag 23 (f_lim, sampler_RHMC.py:194-196), so with
 run_RHMC's f_pos=True every such start has V = inf (sampler_RHMC.py:303-309)
 and every proposal is rejected before any pixel work.  For MH the chains
-start with every flux raised to at least 1.5 f_lim (mag 22.56); the leapfrog
-benches keep the plain starts (the flux wall reflections are part of C3/C5).
+start near the truth (flux x lognormal 2 %, positions +- 0.1 px; seed 2000 +
+shard offset) with every flux raised to at least `floor` f_lim (1.5: mag
+22.56).  The leapfrog benches keep the plain starts (truth x lognormal 10 %,
+0.5 px: the flux-wall reflections are part of C3/C5).
 """
 import re
 
@@ -32,7 +34,7 @@ from .photometry import (default_exp_setup, factors, gauss_PSF, gen_pow_law_samp
 
 
 class Workload:
-    def __init__(self, name, D, q0, p0, params, n_steps, K, note):
+    def __init__(self, name, D, q0, p0, params, n_steps, K, note, truth=None):
         self.name = name
         self.D = D
         self.q0 = q0
@@ -41,6 +43,7 @@ class Workload:
         self.n_steps = n_steps
         self.K = K
         self.note = note
+        self.truth = truth          # multi-star: the image's (f, x, y) per star, counts
 
     @property
     def n_chains(self):
@@ -74,10 +77,21 @@ def _powlaw_stars(rng, K, n, ftc, mag_lo=15., mag_hi=23.3, alpha=2.):
     return f, x, y
 
 
-def mh_start(wl, floor=1.5):
+def mh_start(wl, floor=1.5, seed_offset=0):
     """The workload's chain starts for run_RHMC's MH loop with f_pos=True:
-    fluxes raised to >= floor * f_lim (positions and momenta unchanged)."""
-    q = wl.q0.copy()
+    multi-star workloads near the truth (flux x lognormal 2 %, 0.1 px), every
+    flux raised to >= floor * f_lim; one-star workloads keep q0 (mag 19, far
+    above the wall) with the same floor."""
+    if wl.truth is None:
+        q = wl.q0.copy()
+    else:
+        ft, xt, yt = wl.truth
+        rng = np.random.RandomState(2000 + seed_offset)
+        n = wl.n_chains
+        q = np.empty_like(wl.q0)
+        q[:, 0::3] = ft * np.exp(0.02 * rng.randn(n, wl.K))
+        q[:, 1::3] = xt + 0.1 * rng.randn(n, wl.K)
+        q[:, 2::3] = yt + 0.1 * rng.randn(n, wl.K)
     q[:, 0::3] = np.maximum(q[:, 0::3], floor * wl.params["f_lim"])
     return q
 
@@ -86,6 +100,7 @@ def make(name, n_chains=None, seed_offset=0):
     name = name.upper()
     img_rng = np.random.RandomState(77)
     rng = np.random.RandomState(1000 + seed_offset)
+    truth = None
     if name in ("C1", "C2", "C4"):
         n = 32 if name == "C1" else 48
         par, ftc = base_params(dt=0.1)
@@ -126,9 +141,11 @@ def make(name, n_chains=None, seed_offset=0):
         q0[:, 1::3] = xt + 0.5 * rng.randn(nc, K)
         q0[:, 2::3] = yt + 0.5 * rng.randn(nc, K)
         steps = 500 if name[0] == "C" else 100
+        truth = (ft, xt, yt)
     else:
         raise ValueError("unknown workload " + name)
     H = metric_diag(q0, par)
     p0 = rng.randn(*q0.shape) * np.sqrt(H)
     note = "%s: %dx%d image, K=%d, %d chains, %d steps" % (name, n, n, K, nc, steps)
-    return Workload(name, D, q0, p0, par, steps, K, note)
+    return Workload(name, D, q0, p0, par, steps, K, note,
+                    truth=truth if K > 1 or name[0] != "C" else None)

@@ -11,15 +11,29 @@
  * (:1045), the grow/shrink choice (:1094, :1140), the move's own draws
  * (:1219-1221, :1231, :1249, :1291, :1300-1302, :1328, :1333, :1415) and the
  * accept uniform (:1075, :1164) — so the draws are the reference's bit for
- * bit.  The per-chain host work (metric, kinetic energy, the proposals and
- * their ln-acceptance factors) runs on a pool of host threads; every
- * trajectory and potential of an iteration phase is one engine call per
- * distinct star count (chains grouped by K in order of first appearance,
- * ascending chain index inside a group — with n_pipes = 1 the grouping of the
- * Python multi_gym.run_RHMC_rj_batched, so both see identical engine
- * batches), the groups of a phase on concurrent HIP streams (through
- * rhmc_leapfrog_device / rhmc_energy_device, the entry points rhmc.h allows
- * from several threads at once).
+ * bit.
+ *
+ * rhmc_rj_run keeps the chains in HBM for the whole run (round 5): every
+ * chain's state, iteration-start state and momentum are rows of padded
+ * [n][3 N_max] device arrays, and per iteration only the host-drawn normals,
+ * a few doubles per chain (T, V), the jumping chains' rows (their proposals
+ * run on the host, on a pool of host threads) and — when recorded — the
+ * q_chain / p_chain rows cross PCIe.  The momentum p = z sqrt(H(q)) and both
+ * kinetic energies run on the device (rhmc_kinetic_rows_device); every phase
+ * is one ragged launch per register-slot class for the star counts the
+ * slotted kernels serve (rhmc_leapfrog_ragged_device /
+ * rhmc_energy_ragged_device: the dense kernel from 11 stars on 32/48-px
+ * images, the windowed kernel) plus one packed launch per other star count
+ * (gathered by rhmc_rows_copy_device).  The engine's results do not depend on
+ * the batch a chain is in, so the records equal those of one run_RHMC per
+ * seed.  rhmc_rj_run_physics runs the same iteration on host arrays around
+ * caller-supplied engine callbacks (stand-ins for tests), one call per
+ * distinct star count and phase.
+ *
+ * Concurrency: each pipe of a run uses process-lifetime device buffers and two
+ * HIP streams of its own, held (a mutex) for the whole run, so concurrent
+ * rhmc_rj_run calls on one device serialise pipe by pipe; the caller's
+ * current device is restored on return.
  *
  * Replaces: the per-chain Python loop of run_RHMC's reversible-jump branches
  * (one chain, one star count at a time) — this is its batched, native form.
@@ -119,7 +133,12 @@ typedef struct rhmc_rj_record {
   double* phase_s;   /* [7] wall seconds summed over the run (and over the
                         pipes): momentum + move draws (host), V(q), first
                         trajectories, proposals (host), second
-                        trajectories, V(q'), accept (host)                */
+                        trajectories, V(q'), accept (host).  rhmc_rj_run
+                        overlaps device and host work, so its phases are
+                        the host's waits: [1] momentum / T / V(q) and the
+                        record rows, [2] the first trajectories, [4] only
+                        queueing the second ones, [5] their completion
+                        with V(q') and T'                                   */
 } rhmc_rj_record;
 
 #define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */
