@@ -355,13 +355,13 @@ def bench_rj(args, wl, gpu, world, rank):
     g.device = gpu
     seeds = [1000 * rank + c for c in range(n_chains)]
     for _ in range(args.warmup):
-        g.run_RHMC_rj_batched([m.copy() for m in starts], seeds, n_pipes=args.rj_pipes, **kw)
+        g.run_RHMC_rj_batched(starts, seeds, n_pipes=args.rj_pipes, **kw)
     if world > 1:
         dist.barrier()
     steps = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
-        g.run_RHMC_rj_batched([m.copy() for m in starts], [s + 7 * (i + 1) for s in seeds],
+        g.run_RHMC_rj_batched(starts, [s + 7 * (i + 1) for s in seeds],      # (starts unchanged)
                               n_pipes=args.rj_pipes, **kw)
         # move 0: one trajectory; a jump: two, unless its proposal was a dead end
         steps += int(np.sum(np.where((g.move_chain == 0) | (g.flag_chain != 0), 1, 2))) * leap

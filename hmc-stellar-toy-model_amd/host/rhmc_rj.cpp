@@ -385,17 +385,25 @@ struct Run {
     }
     const int64_t n = c.K;
     if (n - 1 < 1) return false;
-    // pair probabilities ~ Beta(F_ij) N(r_ij), self pairs excluded (:1366-1378)
+    // pair probabilities ~ Beta(F_ij) N(r_ij), self pairs excluded (:1366-1378).
+    // R_sq is symmetric bit for bit ((a - b)^2 == (b - a)^2), so each pair's
+    // Gaussian factor is evaluated once for both orders
     std::vector<double> P2((size_t)(n * n));
     for (int64_t r = 0; r < n; ++r)
-      for (int64_t s = 0; s < n; ++s) {
-        const double fr = c.q[3 * r], fc = c.q[3 * s];
-        const double Fm = fc / (fr + fc);
-        double v = beta.pdf(Fm);
-        if (std::fabs(Fm - 0.5) < 1e-6) v = 0.;
+      for (int64_t s = r; s < n; ++s) {
         const double ddx = c.q[3 * r + 1] - c.q[3 * s + 1], ddy = c.q[3 * r + 2] - c.q[3 * s + 2];
         const double Rsq = std::pow(ddx, 2) + std::pow(ddy, 2);
-        P2[r * n + s] = v * (std::exp(-Rsq / two_ks2) / two_pi_ks2);
+        const double g = std::exp(-Rsq / two_ks2) / two_pi_ks2;
+        const double fr = c.q[3 * r], fc = c.q[3 * s];
+        const double F1 = fc / (fr + fc);
+        double v1 = beta.pdf(F1);
+        if (std::fabs(F1 - 0.5) < 1e-6) v1 = 0.;
+        P2[r * n + s] = v1 * g;
+        if (s == r) continue;
+        const double F2 = fr / (fc + fr);
+        double v2 = beta.pdf(F2);
+        if (std::fabs(F2 - 0.5) < 1e-6) v2 = 0.;
+        P2[s * n + r] = v2 * g;
       }
     const double tot = rhmc_np::pairwise_sum(P2.data(), n * n);
     if (!(tot > 0.0) || !std::isfinite(tot)) return false;  // the reference raises here
