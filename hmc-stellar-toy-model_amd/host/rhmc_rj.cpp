@@ -1288,10 +1288,12 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
 }
 
 int pipes_for(const rhmc_rj_config* cfg, int64_t n) {
-  // default: measured at big-sim4 geometry (profiles/r04_pipes2/): 2 pipes
-  // from 1,024 chains (1.11x one at 4,096; 3 and 4 lose there), 3 from 16,384
-  // (1.54x one, 1.16x two or four)
-  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes : (n >= 16384 ? 3 : n >= 1024 ? 2 : 1);
+  // default for the device-resident driver, measured at big-sim4 geometry
+  // (profiles/r05_pipes/, three repeats on one box, chain-steps/s): 4,096
+  // chains 1.70e7 / 1.82e7 / 1.84e7 with 2 / 3 / 4 pipes; 16,384 chains
+  // 1.80e7 / 2.06e7 / 2.12e7; the flagship (K from 5) 0.99e7 / 1.09e7 / 1.05e7
+  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes
+                               : (n >= 16384 ? 4 : n >= 2048 ? 3 : n >= 1024 ? 2 : 1);
   return (int)std::max<int64_t>(1, std::min<int64_t>(pipes, n));
 }
 

@@ -705,8 +705,8 @@ class multi_gym(base_class):
         threads (0: up to 16) with a bit-identical replica of each chain's
         NumPy stream, and flag_chain [Niter+1, n] marks the iterations whose
         proposal was a dead end (see the header); n_pipes = 2..4 (the default:
-        2 from 1,024 chains, 3 from 16,384) runs the chains in that many parts whose host
-        and GPU phases overlap, 1 keeps the engine batches of the NumPy loop;
+        2 from 1,024 chains, 3 from 2,048, 4 from 16,384) runs the chains in
+        that many parts whose host and GPU phases overlap, 1 in one pass;
         rng_states (native only): the chains' streams to start from instead of
         the seeds — a list of numpy RandomState objects or the rj_rng_states
         array an earlier run left (run it from that run's final q: the draws of
