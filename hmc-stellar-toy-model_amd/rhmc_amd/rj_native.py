@@ -142,12 +142,21 @@ def pack_starts(q_models, N_max, flux_to_count=0.):
     mag2flux (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 —
     or flat flux-count vectors with flux_to_count = 0."""
     n = len(q_models)
-    K = np.fromiter((np.size(m) // 3 for m in q_models), dtype=np.int32, count=n)
-    if n and (K.min() < 1 or K.max() > N_max or
-              any(np.size(m) % 3 for m in q_models)):
-        raise ValueError("every start needs 1 .. N_max stars (3 values each)")
-    rows = np.ascontiguousarray(np.concatenate([np.ravel(m) for m in q_models])
-                                if n else np.zeros(0), dtype=np.float64)
+    if n == 0:
+        return np.zeros((0, 3 * int(N_max))), np.zeros(0, np.int32)
+    flat = [np.asarray(m, dtype=np.float64) for m in q_models]
+    if all(m.ndim == 2 and m.shape[1] == 3 for m in flat):      # [K, 3] rows
+        K = np.fromiter((len(m) for m in flat), dtype=np.int32, count=n)
+        rows = np.concatenate(flat)
+    else:                                                       # flat [3K] vectors
+        sizes = np.fromiter((m.size for m in flat), dtype=np.int64, count=n)
+        if (sizes % 3).any():
+            raise ValueError("a flat q holds 3 values per star")
+        K = (sizes // 3).astype(np.int32)
+        rows = np.concatenate([m.ravel() for m in flat])
+    if K.min() < 1 or K.max() > N_max:
+        raise ValueError("every start needs 1 .. N_max stars")
+    rows = np.ascontiguousarray(rows, dtype=np.float64)
     q = np.empty((n, 3 * int(N_max)))
     _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
                                     float(flux_to_count), q.ctypes.data))
@@ -245,4 +254,5 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
             raise err[0]
         _check(rc)
     flat = q[np.arange(W)[None, :] < 3 * K[:, None]]     # the chains' final q, row after row
-    return np.split(flat, np.cumsum(3 * K.astype(np.int64))[:-1]) if n else [], rec
+    ends = np.cumsum(3 * K.astype(np.int64)).tolist()
+    return [flat[a:b] for a, b in zip([0] + ends[:-1], ends)], rec
