@@ -1384,21 +1384,47 @@ int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t
   if (n < 0 || N_max < 1) return fail(RHMC_ERR_ARG, "bad n or N_max");
   if (n > 0 && (!rows || !K || !q)) return fail(RHMC_ERR_ARG, "rows, K or q is NULL");
   const int64_t W = 3 * (int64_t)N_max;
-  int64_t at = 0;
-  for (int64_t c = 0; c < n; ++c)
-    if (K[c] < 1 || K[c] > N_max) return fail(RHMC_ERR_ARG, "K[c] must be in [1, N_max]");
-  for (int64_t c = 0; c < n; ++c) {
-    double* row = q + c * W;
-    for (int32_t k = 0; k < K[c]; ++k, at += 3) {
-      const double v = rows[at];
-      // mag2flux_converter (sampler_RHMC.py:147-152, utils.py:24-25): libm pow,
-      // the function NumPy's and Python's float power call
-      row[3 * k] = flux_to_count > 0 ? std::pow(10.0, 0.4 * (22.5 - v)) * flux_to_count : v;
-      row[3 * k + 1] = rows[at + 1];
-      row[3 * k + 2] = rows[at + 2];
-    }
-    std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
+  std::vector<int64_t> at;
+  try {
+    at.resize((size_t)n + 1);
+  } catch (...) {
+    return fail(RHMC_ERR_NOMEM, "pack_starts: out of host memory");
   }
+  at[0] = 0;
+  for (int64_t c = 0; c < n; ++c) {
+    if (K[c] < 1 || K[c] > N_max) return fail(RHMC_ERR_ARG, "K[c] must be in [1, N_max]");
+    at[c + 1] = at[c] + 3 * (int64_t)K[c];
+  }
+  auto pack = [&](int64_t c0, int64_t c1) {
+    for (int64_t c = c0; c < c1; ++c) {
+      double* row = q + c * W;
+      const double* src = rows + at[c];
+      for (int32_t k = 0; k < K[c]; ++k) {
+        const double v = src[3 * k];
+        // mag2flux_converter (sampler_RHMC.py:147-152, utils.py:24-25): libm pow,
+        // the function NumPy's and Python's float power call
+        row[3 * k] = flux_to_count > 0 ? std::pow(10.0, 0.4 * (22.5 - v)) * flux_to_count : v;
+        row[3 * k + 1] = src[3 * k + 1];
+        row[3 * k + 2] = src[3 * k + 2];
+      }
+      std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
+    }
+  };
+  // a few host threads for large batches (one pow per star); chains split in
+  // contiguous ranges, so the result does not depend on the thread count
+  const int64_t work = at[n];
+  const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, work / 60000));
+  std::vector<std::thread> th;
+  for (int t = 1; t < nt; ++t) {
+    const int64_t c0 = n * t / nt, c1 = n * (t + 1) / nt;
+    try {
+      th.emplace_back(pack, c0, c1);
+    } catch (...) {  // no thread: this thread packs the range
+      pack(c0, c1);
+    }
+  }
+  pack(0, nt > 1 ? n / nt : n);
+  for (auto& t : th) t.join();
   return 0;
 }
 

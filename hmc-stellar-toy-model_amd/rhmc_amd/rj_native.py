@@ -165,13 +165,15 @@ def pack_starts(q_models, N_max, flux_to_count=0.):
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0, n_pipes=0, states=None, packed=None):
+        n_threads=0, n_pipes=0, states=None, packed=None, out=None):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
     vectors, or None with packed = (q [n][3 N_max], K [n]) from pack_starts.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
     -> None, in place; for stand-ins).  states: None (streams from the seeds)
     or an array of STATE_DTYPE rows to start from (then seeds may be None).
-    Returns (q list, record dict); record["states"] holds every chain's stream
+    out: optional {"q_chain": a, "p_chain": b} float64 [n_iter+1][n][3 N_max]
+    buffers the records are written into (overwritten in full; others are
+    allocated).  Returns (q list, record dict); record["states"] holds every chain's stream
     at the end (pass it back as `states` to resume)."""
     W = 3 * int(N_max)
     if packed is not None:
@@ -212,7 +214,17 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
                    float(fmin), float(fmax), float(K_split), float(beta_a), float(beta_b), sg,
                    sb, st.ctypes.data if n else None)
     rows_n = int(n_iter) + 1
-    rec = {"q_chain": np.zeros((rows_n, n, W)), "p_chain": np.zeros((rows_n, n, W)),
+
+    def rec_buf(key):
+        # the driver writes every (iteration, chain) row of q_chain / p_chain in
+        # full, zero padding included, so a caller's spare buffer of the right
+        # shape can take the records instead of fresh (page-faulting) memory
+        a = (out or {}).get(key)
+        if (isinstance(a, np.ndarray) and a.shape == (rows_n, n, W) and a.dtype == np.float64
+                and a.flags.c_contiguous and a.flags.writeable):
+            return a
+        return np.zeros((rows_n, n, W))
+    rec = {"q_chain": rec_buf("q_chain"), "p_chain": rec_buf("p_chain"),
            "E_chain": np.zeros((rows_n, n)), "V_chain": np.zeros((rows_n, n)),
            "T_chain": np.zeros((rows_n, n)), "accept": np.zeros((rows_n, n), np.int32),
            "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),

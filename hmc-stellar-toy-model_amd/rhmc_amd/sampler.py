@@ -21,6 +21,8 @@ f_expnt to be set (TypeError otherwise, like the reference).
 
 Out of scope here: plotting (display_image, diagnostics_*).
 """
+import sys
+
 import numpy as np
 
 from . import capi
@@ -868,6 +870,16 @@ class multi_gym(base_class):
         else:
             packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max)
         P = self._params(delta, counter_max, for_energy=True)
+        # the previous run's q_chain / p_chain memory takes this run's records
+        # when nothing but this sampler holds it (no caller reference, no view:
+        # the attribute, `a` and getrefcount's argument) — fresh arrays of this
+        # size cost a page fault per 4 KiB inside the run
+        out = {}
+        for key in ("q_chain", "p_chain"):
+            a = self.__dict__.get(key)
+            if isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3:
+                out[key] = a
+            a = None
         import time
         t0 = time.perf_counter()
         q_end, rec = rj_native.run(
@@ -877,7 +889,9 @@ class multi_gym(base_class):
             schedule_beta=schedule_beta, ctx=self._context(), n_threads=n_threads,
             n_pipes=n_pipes, states=(None if rng_states is None else
                                      rng_states if isinstance(rng_states, np.ndarray)
-                                     else rj_native.states_from(rng_states)), packed=packed)
+                                     else rj_native.states_from(rng_states)), packed=packed,
+            out=out)
+        out = None
         self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
         for name, sched in (("g_ff2", schedule_g_ff2), ("beta", schedule_beta)):

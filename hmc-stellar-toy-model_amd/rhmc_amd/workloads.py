@@ -8,16 +8,17 @@ Every config is a data image plus a batch of chain states (q0, p0):
   C5  256x256, K=64, 8192 chains    (flux-wall RHMC, prior on)
 Beyond BASELINE's configs, the reference's own many-star drivers (dense
 32x32 images, big-sim4 parameters, prior on):
-  B4  32x32, K=51,  4096 chains, 100 steps (RHMC-big-sim4.py: 32**2 * 0.05 stars)
-  B3  32x32, K=100, 4096 chains, 100 steps (RHMC-big-sim3.py: Nobjs = 100)
+  B4  32x32, K=51,  4096 chains, 100 steps (RHMC-big-sim4.py: 32**2 * 0.05 true
+      stars of magnitudes 15 .. 20, :20, :30-31)
+  B3  32x32, K=100, 4096 chains, 100 steps (RHMC-big-sim3.py: Nobjs = 100 of
+      magnitudes 15 .. 20.5, :18, :28-29)
   S<n>K<k>  n x n, K=k, 4096 chains, 100 steps, the same parameters (kernel
             sweeps, e.g. S48K32)
 
 Randomness: numpy legacy RandomState; the image uses seed 77
 (RHMC-big-sim4.py:18), chain initial states seed 1000 (+ shard offset).
 
-MH starts (`mh_start`): the multi-star workloads draw magnitudes down to
-23.3, below the flux wall at mag 23 (f_lim, sampler_RHMC.py:194-196), so with
+MH starts (`mh_start`): C3 and C5 draw magnitudes down to 23.3, below the flux wall at mag 23 (f_lim, sampler_RHMC.py:194-196), so with
 run_RHMC's f_pos=True every such start has V = inf (sampler_RHMC.py:303-309)
 and every proposal is rejected before any pixel work.  For MH the chains
 start near the truth (flux x lognormal 2 %, positions +- 0.1 px; seed 2000 +
@@ -131,7 +132,10 @@ def make(name, n_chains=None, seed_offset=0):
             fmin, fmax = mag2flux(23.3) * ftc, mag2flux(15.) * ftc
             par["V_prior_const"] = np.log(n * n) - np.log(
                 (1 - a) / (fmax ** (1 - a) - fmin ** (1 - a)))
-        ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc)
+        # true magnitudes: down to 23.3 for BASELINE's C3 / C5 (below the flux
+        # wall at 23); the reference drivers' ranges for B4 / B3
+        mag_hi = {"B4": 20., "B3": 20.5}.get(name, 23.3)
+        ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc, mag_hi=mag_hi)
         D = _image(n, [(22.5 - 2.5 * np.log10(a / ftc), b, c) for a, b, c in zip(ft, xt, yt)],
                    ftc, par["B_count"], par["fwhm_pix"], img_rng)
         nc = ({"C3": 16384, "C5": 8192}.get(name, 4096)) if n_chains is None else n_chains

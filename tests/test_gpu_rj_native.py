@@ -137,6 +137,43 @@ def test_native_two_pipes_equal_one(gpu_lib):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
 
 
+def test_native_record_buffers_reused_only_when_unreferenced(gpu_lib):
+    """A second run writes its q_chain / p_chain records into the first run's
+    memory only when nothing but the sampler holds it; the records equal a
+    fresh sampler's either way (every row, padding included, is overwritten),
+    and a caller's reference keeps the first run's records intact."""
+    z = load_golden("rj")
+    name = "rj_all"
+    par = R.params_from_npz(z, name + "/par_")
+
+    def make():
+        g = _gym(par)
+        g.D = z[name + "/D"]
+        return g
+    starts = _starts(z[name + "/q_model"], 24, np.random.RandomState(3))
+    kw = dict(f_pos=True, delta=1e-6, Niter=5, Nsteps=4, dt=0.05, N_max=12,
+              P_move=[0.4, 0.3, 0.3])
+    g = make()
+    g.run_RHMC_rj_batched(starts, list(range(24)), **kw)
+    first = g.q_chain.copy()
+    addr = g.q_chain.ctypes.data
+    g.run_RHMC_rj_batched(starts, list(range(100, 124)), **kw)    # reuses the buffer
+    assert g.q_chain.ctypes.data == addr
+    fresh = make()
+    fresh.run_RHMC_rj_batched(starts, list(range(100, 124)), **kw)
+    np.testing.assert_array_equal(g.q_chain, fresh.q_chain)
+    np.testing.assert_array_equal(g.p_chain, fresh.p_chain)
+    held = g.q_chain                                                # a caller's reference
+    g.run_RHMC_rj_batched(starts, list(range(24)), **kw)
+    assert g.q_chain is not held
+    np.testing.assert_array_equal(g.q_chain, first)
+    np.testing.assert_array_equal(held, fresh.q_chain)
+    view = g.p_chain[1]                                             # a view blocks it too
+    before = view.copy()
+    g.run_RHMC_rj_batched(starts, list(range(100, 124)), **kw)
+    np.testing.assert_array_equal(view, before)
+
+
 def test_native_recorded_V_dense_ragged(gpu_lib):
     """The same V-reuse check where the driver's phases are ragged dense
     launches (32x32, 12 - 40 stars, births and splits past the starting
