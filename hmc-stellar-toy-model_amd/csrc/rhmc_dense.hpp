@@ -86,7 +86,7 @@ struct DenseG {
 
   // Block-wide prologue (every thread of the block, before any early exit).
   static __device__ __forceinline__ Ctx setup(double* lds, const double* __restrict__ D, int,
-                                              int, int) {
+                                              int, int, double* /*work*/) {
     exp_tab_fill(lds);
     double* img = lds + kExpTab;
     for (int e = threadIdx.x; e < IMG * IMG; e += blockDim.x) img[e] = D[e];

@@ -45,6 +45,7 @@ namespace rhmc {
 struct Geometry {
   int rows, cols, npix, npl;  // npl = ceil(npix / 64) pixels per lane
   int di, dj;                 // pixel index step of 64 as (rows, cols)
+  double* work;               // WinGG's per-chain factor tables (K > 256), else null
 };
 
 struct Tables {  // per-wave LDS tables, K stars
@@ -541,7 +542,7 @@ __device__ __forceinline__ void run_steps_win(WinState<SLOTS>& s, int n_steps, i
 template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) leapfrog_win_kernel(LeapArgs a) {
   extern __shared__ double lds[];
-  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols, a.g.work);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
@@ -712,7 +713,7 @@ __device__ __forceinline__ double dVdq_rhmc_f(double f, double pf, const Consts&
 template <class G, int SOLVER, int SLOTS>
 __global__ void __launch_bounds__(256) integrate_win_kernel(LeapArgs a, int f_pos) {
   extern __shared__ double lds[];
-  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols, a.g.work);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
@@ -811,7 +812,7 @@ __global__ void __launch_bounds__(256) hmc_random_win_kernel(LeapArgs a,
                                                              const double* __restrict__ dtv,
                                                              const int32_t* __restrict__ steps) {
   extern __shared__ double lds[];
-  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols, a.g.work);
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
@@ -897,7 +898,7 @@ __device__ __forceinline__ void win_load_q(const double* q, int64_t row, int64_t
 template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
   extern __shared__ double lds[];
-  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols, a.g.work);
   const int W = blockDim.x / kWave;
   const int64_t chain = (int64_t)blockIdx.x * W + (threadIdx.x / kWave);
   if (chain >= a.n_chains) return;
@@ -921,7 +922,7 @@ __global__ void __launch_bounds__(256) gradient_win_kernel(GradArgs a) {
 template <class G, int SLOTS>
 __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   extern __shared__ double lds[];
-  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols);
+  const typename G::Ctx gctx = G::setup(lds, a.D, a.K, a.g.rows, a.g.cols, a.g.work);
   const Geometry& g = a.g;
   const Consts& c = a.c;
   const int W = blockDim.x / kWave;
@@ -1058,10 +1059,37 @@ int window_unsupported() {
 
 
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
-constexpr int kMaxK = 256;         // windowed kernels: 64 lanes x 4 star slots
+constexpr int kMaxKLds = 256;      // slotted kernels, LDS tables: 64 lanes x 4 star slots
+constexpr int kMaxK = 1024;        // slotted kernels, global tables (WinGG): 8 / 16 slots
 
 // Star slots per lane of the windowed kernels for K stars.
-int win_slots(int K) { return K <= 64 ? 1 : (K <= 128 ? 2 : 4); }
+int win_slots(int K) {
+  return K <= 64 ? 1 : K <= 128 ? 2 : K <= 256 ? 4 : K <= 512 ? 8 : 16;
+}
+
+// WinGG's per-chain factor tables (K > 256) for the n chains of one launch:
+// allocated on the launch's stream and released behind it (stream-ordered,
+// so the launch that reads them has finished first).
+struct WorkTables {
+  void* p = nullptr;
+  hipStream_t s = nullptr;
+  int get(int K, int64_t n, hipStream_t st, double** out) {
+    *out = nullptr;
+    if (K <= kMaxKLds || n <= 0) return RHMC_OK;
+    s = st;
+    const size_t bytes = (size_t)n * WinGG::work_doubles(K) * sizeof(double);
+    if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
+      p = nullptr;
+      return fail(RHMC_ERR_NOMEM, "hipMallocAsync of " + std::to_string(bytes) +
+                                      " B of factor tables (K > 256) failed");
+    }
+    *out = (double*)p;
+    return RHMC_OK;
+  }
+  ~WorkTables() {
+    if (p) (void)hipFreeAsync(p, s);
+  }
+};
 
 template <class G, int SLOTS>
 void launch_integrate_win(int32_t solver, dim3 grid, dim3 block, size_t lds, hipStream_t s,
@@ -1092,11 +1120,26 @@ int with_slots(int K, F&& f) {
     default: return f(TypeTag<G>{}, IntTag<4>{});
   }
 }
+// K > 256: the global-table policy at 8 or 16 slots (the only policy
+// instantiated there)
+template <class F>
+int with_big(int K, F&& f) {
+  if (K <= 512) return f(TypeTag<WinGG>{}, IntTag<8>{});
+  return f(TypeTag<WinGG>{}, IntTag<16>{});
+}
 template <class F>
 int with_path(int path, int K, F&& f) {
+  if (K > kMaxKLds) return with_big(K, f);
   if (path == 32) return with_slots<DenseG<32>>(K, f);
   if (path == 48) return with_slots<DenseG<48>>(K, f);
   return with_slots<WinG>(K, f);
+}
+// The windowed energy kernel's policy: column tables only (WinEG) up to 256
+// stars, the global tables above
+template <class F>
+int with_energy_win(int K, F&& f) {
+  if (K > kMaxKLds) return with_big(K, f);
+  return with_slots<WinEG>(K, f);
 }
 
 // Which kernel family serves (K, image): the LDS-image kernels need D and the
@@ -1112,6 +1155,11 @@ bool use_windowed(const rhmc_ctx* ctx, int K) {
 // for one wave, within gfx950's 160 KB; a device with less LDS gets
 // RHMC_ERR_UNSUPPORTED here, not a failed launch).
 int pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
+  if (K > kMaxKLds) {  // WinGG: the exp table only
+    *W = 4;
+    *lds = WinGG::lds_bytes(4, K);
+    return RHMC_OK;
+  }
   int w = 4;
   while (w > 1 && WinG::lds_bytes(w, K) > (size_t)ctx->max_lds) w >>= 1;
   *W = w;
@@ -1150,6 +1198,7 @@ int pick_waves_path(const rhmc_ctx* ctx, int path, int K, size_t* lds, int* W) {
 constexpr int kDenseMinK = 11;
 bool tiledrk_ok(const rhmc_ctx* ctx, int K, const Consts& c);
 int dense_path(const rhmc_ctx* ctx, int K, const Consts& c) {
+  if (K > kMaxKLds) return 0;  // four register slots at most
   if (ctx->rows != ctx->cols || (ctx->rows != 32 && ctx->rows != 48)) return 0;
   if (per_wave_forced(ctx)) return 0;
   if (ctx->kernel != RHMC_KERNEL_DENSE) {
@@ -1169,6 +1218,7 @@ Geometry make_geometry(int rows, int cols) {
   g.npl = (g.npix + kWave - 1) / kWave;
   g.di = kWave / cols;
   g.dj = kWave % cols;
+  g.work = nullptr;
   return g;
 }
 
@@ -1248,7 +1298,7 @@ int check_common(rhmc_ctx* ctx, int64_t n_chains, int32_t K) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   if (!ctx->d_D) return fail(RHMC_ERR_ARG, "no image uploaded");
   if (n_chains < 0) return fail(RHMC_ERR_ARG, "n_chains < 0");
-  if (K < 1 || K > kMaxK) return fail(RHMC_ERR_ARG, "K must be in [1, 256]");
+  if (K < 1 || K > kMaxK) return fail(RHMC_ERR_ARG, "K must be in [1, 1024]");
   if (n_chains > ((int64_t)1 << 40)) return fail(RHMC_ERR_ARG, "n_chains too large");
   return RHMC_OK;
 }
@@ -1436,7 +1486,9 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   const int path = dense_path(ctx, K, c);
   const bool win = path || use_windowed(ctx, K);
   if (win && !path && !window_exact(c)) return window_unsupported();
-  if (win && !path) {  // potential-only windowed tables (WinEG)
+  if (win && !path && K > kMaxKLds) {  // global tables (WinGG)
+    if ((rc = pick_waves_win(ctx, K, &lds, &W))) return rc;
+  } else if (win && !path) {  // potential-only windowed tables (WinEG)
     W = 4;
     while (W > 1 && WinEG::lds_bytes(W, K) > (size_t)ctx->max_lds) W >>= 1;
     lds = WinEG::lds_bytes(W, K);
@@ -1456,6 +1508,8 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.K = K;
   a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
   a.g = make_geometry(ctx->rows, ctx->cols);
+  WorkTables wt;
+  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
     auto go = [&](auto gt, auto st) {
@@ -1464,7 +1518,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
       HIP_TRY(hipGetLastError());
       return (int)RHMC_OK;
     };
-    return path ? with_path(path, K, go) : with_slots<WinEG>(K, go);
+    return path ? with_path(path, K, go) : with_energy_win(K, go);
   }
   return dispatch_k<EnergyLaunch>(K, grid, block, lds, s, a);
 }
@@ -1662,6 +1716,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.K = K;
     a.n_steps = n_steps;
     if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
+    WorkTables wt;
+    if ((rc = wt.get(K, n_chains, s, &a.g.work))) return rc;
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
     return with_path(path, K, [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
@@ -1708,10 +1764,10 @@ int ragged_family(const rhmc_ctx* ctx, const Consts& c, int K) {
 int ragged_check(const rhmc_ctx* ctx, const Consts& c, int K_min, int K_max, int64_t ld,
                  int* family) {
   if (K_min < 1 || K_max > kMaxK || K_min > K_max)
-    return fail(RHMC_ERR_ARG, "ragged set: need 1 <= K_min <= K_max <= 256");
+    return fail(RHMC_ERR_ARG, "ragged set: need 1 <= K_min <= K_max <= 1024");
   if (win_slots(K_min) != win_slots(K_max))
     return fail(RHMC_ERR_ARG, "ragged set: K_min and K_max need the same register slots "
-                              "(1-64, 65-128, 129-256 stars)");
+                              "(1-64, 65-128, 129-256, 257-512, 513-1024 stars)");
   if (ld < 3 * (int64_t)K_max) return fail(RHMC_ERR_ARG, "ragged set: ld < 3 K_max");
   const int f = ragged_family(ctx, c, K_min);
   for (int K = K_min; K <= K_max; ++K)
@@ -1751,6 +1807,8 @@ int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, dou
   size_t lds;
   int W;
   if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
+  WorkTables wt;
+  if ((rc = wt.get(K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K_max, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -1773,7 +1831,7 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   const int path = dense_path(ctx, K_max, a.c);
   size_t lds;
   int W;
-  if (path) {
+  if (path || K_max > kMaxKLds) {
     if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
   } else {  // potential-only windowed tables, as launch_energy
     W = 4;
@@ -1794,6 +1852,8 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   a.Kc = d_K;
   a.rows = d_rows;
   a.ld = ld;
+  WorkTables wt;
+  if ((rc = wt.get(K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   auto go = [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -1801,7 +1861,7 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
     HIP_TRY(hipGetLastError());
     return (int)RHMC_OK;
   };
-  return path ? with_path(path, K_max, go) : with_slots<WinEG>(K_max, go);
+  return path ? with_path(path, K_max, go) : with_energy_win(K_max, go);
 }
 
 // One star where launch_leapfrog takes the register-window kernel (28-px
@@ -2164,6 +2224,8 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
+  WorkTables wt;
+  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
   return with_path(path, K, [&](auto gt, auto st) {
@@ -2267,6 +2329,8 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
+  WorkTables wt;
+  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2631,6 +2695,8 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.K = K;
   a.with_metric = kind;
   a.g = make_geometry(ctx->rows, ctx->cols);
+  WorkTables wt;
+  if ((rc = wt.get(K, n_chains, ctx->stream, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
     rc = with_path(path, K, [&](auto gt, auto st) {

@@ -1,4 +1,4 @@
-// rhmc_windowed.hpp — the catch-all path: any square image, 1 <= K <= 256
+// rhmc_windowed.hpp — the catch-all path: any square image, 1 <= K <= 1024
 // stars per chain (lanes = stars, SLOTS stars per lane).
 //
 // The reference evaluates every star's PSF on the full image (sampler_RHMC.py
@@ -13,7 +13,10 @@
 // Stars.  One wave per chain; star k lives in lane k % 64, register slot
 // k / 64 (SLOTS = 1, 2, 4: K <= 64, 128, 256 — the reference takes any
 // 3 * Nobjs, and its own drivers run K = 100 and grow K to N_max = 120 by
-// births: RHMC-big-sim3.py:18-19, RHMC-big-sim4.py:77).
+// births: RHMC-big-sim3.py:18-19, RHMC-big-sim4.py:77).  Beyond 256 stars
+// (SLOTS = 8, 16: K <= 512, 1024) the tables no longer fit LDS and live in
+// global memory (WinGG below); those register states spill to scratch — a
+// completeness path, not a tuned one.
 //
 // Gradient, star-major: for star k (wave-uniform), lane (r = l>>5, c = l&31)
 // owns window column c and rows r, r+2, .., r+30 (16 pixels); Lambda at those
@@ -50,13 +53,27 @@ __device__ __forceinline__ int readlane_i(int v, int src) {
   return __builtin_amdgcn_readlane(v, src);
 }
 
+// The wave's table writes visible to its own later reads: LDS tables need
+// only the wavefront-scope ordering; tables in global memory (GT) a
+// workgroup-scope fence, which waits for the stores.
+template <bool GT>
+__device__ __forceinline__ void tab_sync() {
+  if constexpr (GT) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  } else {
+    wave_lds_sync();
+  }
+}
+
 // Does lane `lane` hold a star in slot t?
 __device__ __forceinline__ bool win_own(int t, int K) { return kWave * t + lane_id() < K; }
 
 // Windowed PSF factor tables for K stars (star 64 t + l in lane l, slot t);
 // the entries of a slot are flattened over (star, axis, index) so all 64 lanes
 // work.
-template <int SLOTS>
+template <int SLOTS, bool GT = false>
 __device__ __forceinline__ void win_build_tables(const WinTables& t, int K,
                                                  const double (&x)[SLOTS],
                                                  const double (&y)[SLOTS], const int (&bx)[SLOTS],
@@ -92,7 +109,7 @@ __device__ __forceinline__ void win_build_tables(const WinTables& t, int K,
       }
     }
   }
-  wave_lds_sync();
+  tab_sync<GT>();
 }
 
 // Repulsion gradient (sampler_RHMC.py:411-418), lanes = stars: every star of
@@ -123,7 +140,7 @@ __device__ __forceinline__ void vc_gradient(int K, const double (&x)[SLOTS],
 
 // dVdq (+ dphidq metric term) of the wave's chain; lane l gets star 64 s + l's
 // in slot s.
-template <int SLOTS>
+template <int SLOTS, bool GT = false>
 __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, int K,
                              const double (&f)[SLOTS], const double (&x)[SLOTS],
                              const double (&y)[SLOTS], int rows, int cols, const Consts& c,
@@ -137,7 +154,7 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
     by[s] = win_base(y[s]);
     gf[s] = gx[s] = gy[s] = 0.0;
   }
-  win_build_tables<SLOTS>(t, K, x, y, bx, by, lc);
+  win_build_tables<SLOTS, GT>(t, K, x, y, bx, by, lc);
   const int lrow = lane >> 5, lcol = lane & 31;
 
 #pragma unroll
@@ -230,13 +247,13 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
     if (with_metric) gf[s] += metric_flux_term(f[s], c);    // :459-463
   }
   if (c.use_Vc) vc_gradient<SLOTS>(K, x, y, c, gx, gy);     // :411-418
-  wave_lds_sync();
+  tab_sync<GT>();
 }
 
 // Column factor tables only (the potential's; the row factors are per-row
 // scalars there): ey [K][kTabW], flattened over (star, index) like
 // win_build_tables.
-template <int SLOTS>
+template <int SLOTS, bool GT = false>
 __device__ __forceinline__ void win_build_ey(double* ey, int K, const double (&y)[SLOTS],
                                              const int (&by)[SLOTS], const LeanConsts& lc) {
   const int lane = lane_id();
@@ -263,7 +280,7 @@ __device__ __forceinline__ void win_build_ey(double* ey, int K, const double (&y
       }
     }
   }
-  wave_lds_sync();
+  tab_sync<GT>();
 }
 
 // e[l] = exp(-c (v0 + l)^2), l < 8: by recurrence from two exps when v0 is
@@ -303,7 +320,7 @@ __device__ __forceinline__ void gauss_run8(double v0, double scale, const double
 // within 2 ulp, ~25 VALU).
 constexpr int kPotRows = 8;  // a multiple of 8 (gauss_run8)
 
-template <int SLOTS>
+template <int SLOTS, bool GT = false>
 __device__ double win_potential(const double* __restrict__ D, double* ey,
                                 const double* __restrict__ etab, int K,
                                 const double (&f)[SLOTS], const double (&x)[SLOTS],
@@ -317,7 +334,7 @@ __device__ double win_potential(const double* __restrict__ D, double* ey,
     bx[s] = win_base(x[s]);
     by[s] = win_base(y[s]);
   }
-  win_build_ey<SLOTS>(ey, K, y, by, lc);
+  win_build_ey<SLOTS, GT>(ey, K, y, by, lc);
   const double lnB = log_pos(c.B);
   double v = 0.0;
   for (int i0 = 0; i0 < rows; i0 += R) {
@@ -393,7 +410,7 @@ __device__ double win_potential(const double* __restrict__ D, double* ey,
         v += (jin && r < nr) ? lam[r] - d[r] * lg[r] : 0.0;
     }
   }
-  wave_lds_sync();
+  tab_sync<GT>();
   return wave_sum_dpp(v);
 }
 
@@ -410,7 +427,7 @@ struct WinG {
     int rows, cols;
   };
   static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
-                                              int cols) {
+                                              int cols, double* /*work*/) {
     exp_tab_fill(lds);
     __syncthreads();
     double* base = lds + kExpTab + (threadIdx.x / kWave) * win_table_doubles(K);
@@ -455,7 +472,7 @@ struct WinEG {
     int rows, cols;
   };
   static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
-                                              int cols) {
+                                              int cols, double* /*work*/) {
     exp_tab_fill(lds);
     __syncthreads();
     Ctx g;
@@ -473,6 +490,50 @@ struct WinEG {
                                                      const double (&y)[SLOTS], const Consts& c,
                                                      const LeanConsts& lc) {
     return win_potential<SLOTS>(g.D, g.ey, g.etab, K, f, x, y, g.rows, g.cols, c, lc);
+  }
+};
+
+// K > 256 (SLOTS 8 / 16): WinG's gradient and potential with each chain's
+// factor tables in global memory — work + (launch wave) x 2 K 33 doubles,
+// 0.5 MB per chain at K = 1024, allocated by the launcher on the launch's
+// stream (Geometry::work) — and only the exp table in LDS.  The tables stay
+// in L2 / HBM, the state spills: correctness at any star count the windowed
+// bound allows, not a tuned kernel (the reference's drivers stop at 120).
+struct WinGG {
+  static __host__ __device__ size_t lds_bytes(int, int) { return kExpTab * sizeof(double); }
+  static __host__ __device__ size_t work_doubles(int K) { return win_table_doubles(K); }
+  using Ctx = WinG::Ctx;
+  static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
+                                              int cols, double* work) {
+    exp_tab_fill(lds);
+    __syncthreads();
+    const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
+    double* base = work + wave * (int64_t)win_table_doubles(K);
+    Ctx g;
+    g.etab = lds;
+    g.tab = WinTables{base, base + K * kTabW};
+    g.D = D;
+    g.rows = rows;
+    g.cols = cols;
+    return g;
+  }
+  template <int SLOTS>
+  static __device__ __forceinline__ void gradient(const Ctx& g, int K, const double (&f)[SLOTS],
+                                                  const double (&x)[SLOTS],
+                                                  const double (&y)[SLOTS], const Consts& c,
+                                                  const LeanConsts& lc, bool with_metric,
+                                                  double (&gf)[SLOTS], double (&gx)[SLOTS],
+                                                  double (&gy)[SLOTS]) {
+    win_gradient<SLOTS, true>(g.D, g.tab, K, f, x, y, g.rows, g.cols, c, lc, with_metric, gf, gx,
+                              gy);
+  }
+  template <int SLOTS>
+  static __device__ __forceinline__ double potential(const Ctx& g, int K,
+                                                     const double (&f)[SLOTS],
+                                                     const double (&x)[SLOTS],
+                                                     const double (&y)[SLOTS], const Consts& c,
+                                                     const LeanConsts& lc) {
+    return win_potential<SLOTS, true>(g.D, g.tab.ex, g.etab, K, f, x, y, g.rows, g.cols, c, lc);
   }
 };
 

@@ -210,8 +210,12 @@ int rhmc_ctx_synchronize(rhmc_ctx* ctx);
  * n_steps RHMC_single_step()s on every chain.  q, p: host [n_chains][3K],
  * updated in place.  fp_iters (nullable): host int32 [n_chains][2], the
  * p- and q-loop iteration counts summed over the n_steps steps.  status
- * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 256 on
- * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).
+ * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 1024 on
+ * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).  Past
+ * 256 stars the one-wave-per-chain kernels keep their windowed PSF factor
+ * tables in global memory, 2 x 33 doubles per star per chain allocated on the
+ * call's stream for the launch (RHMC_ERR_NOMEM if that fails), and need a
+ * PSF narrow enough for the 32-pixel window (else RHMC_ERR_UNSUPPORTED).
  */
 int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p,
                   int64_t n_chains, int32_t K, int32_t n_steps,
@@ -230,8 +234,8 @@ int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
  * star count in [K_min, K_max] when the automatic dispatch runs a slotted
  * one-wave-per-chain kernel for each of them — the dense kernel on 32/48-px
  * images from 11 stars, the windowed kernel (rhmc_ragged_ok says which K);
- * K_min and K_max must need the same register slots (1-64, 65-128, 129-256
- * stars), else RHMC_ERR_ARG, and a K the slotted kernels do not serve gives
+ * K_min and K_max must need the same register slots (1-64, 65-128, 129-256,
+ * 257-512, 513-1024 stars), else RHMC_ERR_ARG, and a K the slotted kernels do not serve gives
  * RHMC_ERR_UNSUPPORTED.  Each chain's results equal those of a fixed-K call
  * on it (the kernels are batch-invariant).  Asynchronous on `stream`.
  */

@@ -847,6 +847,55 @@ def case_flagship(S, U):
     return {"flagship": out}
 
 
+def case_hugek(S, U):
+    """K > 256 stars per chain: the engine's slotted kernels with their factor
+    tables in global memory (8 register slots up to 512 stars, 16 up to
+    1024).  The reference's dVdq / V / RHMC_single_step are vectorised over
+    any K (sampler_RHMC.py:365-425, :294-351, :522-566).
+
+    hugek.npz: per-function vectors (dVdq, dphidq, V, T, H) at K = 300 (64 px)
+    and K = 700 (128 px), big-sim4 parameters + prior, 3 states each.
+    traj_hugek.npz: 1 chain x 3 steps at 64 px, K = 300; traj_hugek700.npz:
+    1 chain x 2 steps at 128 px, K = 700."""
+    out = {}
+    rs = np.random.RandomState(9)
+    for name, n, K in (("h300", 64, 300), ("h700", 128, 700)):
+        np.random.seed(77)
+        g = make_gym(S, n=n, g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True)
+        stars = powlaw_stars(U, g, K, n)
+        g.gen_mock_data(np.array(stars))
+        g.Nobjs, g.d = K, 3 * K
+        q_true = stars_to_q(g, stars)
+        qs, ps = [], []
+        for t in range(3):
+            q = q_true.copy()
+            q[0::3] *= np.exp(0.2 * rs.randn(K))
+            q[1::3] += 0.5 * rs.randn(K)
+            q[2::3] += 0.5 * rs.randn(K)
+            qs.append(q)
+            ps.append(rs.randn(3 * K) * np.sqrt(np.abs(g.H(q))))
+        qs, ps = np.array(qs), np.array(ps)
+        res = dict(D=g.D, q=qs, p=ps)
+        res["dVdq"] = np.array([g.dVdq(q) for q in qs])
+        res["H"] = np.array([g.H(q) for q in qs])
+        res["dphidq"] = np.array([g.dphidq(q) for q in qs])
+        res["V"] = np.array([g.V(q, f_pos=False) for q in qs])
+        res["Vpos"] = np.array([g.V(q, f_pos=True) for q in qs])
+        res["T"] = np.array([g.T(p, g.H(q)) for q, p in zip(qs, ps)])
+        out.update(pack(name + "/", res))
+        out.update(pack(name + "/par_", gym_params(g)))
+        print("hugek", name, "done")
+    cases = {"hugek": out}
+    big = dict(g_xx=0.05, g_ff=4., g_ff2=4., dt=0.05, prior=True)
+    cases["traj_hugek"] = traj_case(
+        S, U, 64, lambda g: powlaw_stars(U, g, 300, 64),
+        lambda g, c: powlaw_stars(U, g, 300, 64), big, 1, 3)
+    cases["traj_hugek700"] = traj_case(
+        S, U, 128, lambda g: powlaw_stars(U, g, 700, 128),
+        lambda g, c: powlaw_stars(U, g, 700, 128), big, 1, 2)
+    return cases
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
@@ -877,8 +926,9 @@ def main():
             print("wrote mh_bigk")
         # subsets of the above, regenerated on their own (--only c5 / bigk)
         for job, fn in (("c5", case_c5), ("bigk", case_bigk), ("flagship", case_flagship),
-                        ("rj_big", case_rj_big)):
-            if args.only == job or (not args.only and job in ("bigk", "flagship", "rj_big")):
+                        ("rj_big", case_rj_big), ("hugek", case_hugek)):
+            if args.only == job or (not args.only and job in ("bigk", "flagship", "rj_big",
+                                                              "hugek")):
                 for name, d in fn(S, U).items():
                     np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
                     print("wrote", name)

@@ -235,8 +235,8 @@ static void gpu_checks() {
         for (int i = 0; i < 6; ++i) fin = fin && std::isfinite(q[c * 6 + i]) && std::isfinite(p[c * 6 + i]);
         CHECK(fin == !(st[c] & RHMC_STATUS_NONFINITE), "NONFINITE flag 32 px chain %d", c);
       }
-      CHECK(rhmc_leapfrog(ctx, &P, q.data(), p.data(), 9, 257, 1, nullptr, nullptr) ==
-                RHMC_ERR_ARG, "K = 257 rejected");
+      CHECK(rhmc_leapfrog(ctx, &P, q.data(), p.data(), 9, 1025, 1, nullptr, nullptr) ==
+                RHMC_ERR_ARG, "K = 1025 rejected");
       rhmc_params bad = P;
       bad.reserved = 1;
       CHECK(rhmc_leapfrog(ctx, &bad, q.data(), p.data(), 9, 2, 1, nullptr, nullptr) ==

@@ -2,7 +2,7 @@
 drivers run K = 100 (RHMC-big-sim3.py:18-19) and grow K by births up to
 N_max = 120 (RHMC-big-sim4.py:77); its dVdq / V / RHMC_single_step take any
 3 * Nobjs (sampler_RHMC.py:365-425, :294-351, :522-566).  The engine takes
-1 <= K <= 256.  Every test runs on the automatic choice (32/48-px images: the
+1 <= K <= 1024 (past 256: tests/test_gpu_hugek.py).  Every test runs on the automatic choice (32/48-px images: the
 dense many-star kernel, rhmc_dense.hpp; 256 px: the windowed kernel) and
 with each family forced.
 
@@ -254,8 +254,8 @@ def test_bigk_mh_vs_oracle(gpu_lib, bigk_kernel):
 
 
 def test_k256_limit(gpu_lib, bigk_kernel):
-    """K = 256 (four star slots per lane) runs and matches the oracle; K = 257
-    is rejected with RHMC_ERR_ARG."""
+    """K = 256 (four star slots per lane, the last LDS-table count) runs and
+    matches the oracle; K = 1025 is rejected with RHMC_ERR_ARG."""
     capi = gpu_lib
     z = load_golden("traj_bigk")
     par = R.params_from_npz(z)
@@ -280,7 +280,7 @@ def test_k256_limit(gpu_lib, bigk_kernel):
         assert_state_close(q1[c], qo, 1e-10, "K=256 q")
         assert_state_close(p1[c], po, 1e-9, "K=256 p")
     with pytest.raises(capi.RhmcError):
-        ctx.leapfrog(P, np.ones((1, 3 * 257)), np.zeros((1, 3 * 257)), 1)
+        ctx.leapfrog(P, np.ones((1, 3 * 1025)), np.zeros((1, 3 * 1025)), 1)
     ctx.close()
 
 

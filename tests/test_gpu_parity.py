@@ -195,7 +195,7 @@ def test_errors(gpu_lib):
     ctx = _ctx(capi, z)
     P = capi_params(capi, par)
     with pytest.raises(capi.RhmcError):
-        ctx.leapfrog(P, np.zeros((2, 3 * 257)), np.zeros((2, 3 * 257)), 1)   # K > 256
+        ctx.leapfrog(P, np.zeros((2, 3 * 1025)), np.zeros((2, 3 * 1025)), 1)   # K > 1024
     with pytest.raises((capi.RhmcError, ValueError)):
         ctx.gradient(P, np.zeros((2, 0)))                                # K = 0
     bad = capi_params(capi, par)
