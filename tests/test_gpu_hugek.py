@@ -78,7 +78,7 @@ def _case(K, n_img, n_chains, seed, flux_floor=1.5):
     """A power-law image of K true stars (mags 15-20, every flux above the
     wall) and n_chains chains at the truth, jittered."""
     z = load_golden("traj_hugek")
-    par = R.params_from_npz(z)
+    par = dict(R.params_from_npz(z), rows=n_img, cols=n_img)
     rs = np.random.RandomState(seed)
     ftc = par["flux_to_count"]
     fmin, fmax = R.mag2flux(20.) * ftc, R.mag2flux(15.) * ftc
