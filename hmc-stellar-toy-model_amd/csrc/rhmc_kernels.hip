@@ -2630,7 +2630,11 @@ int rhmc_kinetic_rows_device(rhmc_ctx* ctx, const rhmc_params* P, const double* 
   a.g2 = P->g2;
   a.B = P->B_count;
   a.f_low = P->f_low;
-  hipLaunchKernelGGL(kinetic_rows_kernel, dim3((unsigned)((n + 3) / 4)), dim3(256), 0, s, a);
+  if (ld <= 768)  // up to 256 stars: four chains per block
+    hipLaunchKernelGGL((kinetic_rows_kernel<4, 768, 3>), dim3((unsigned)((n + 3) / 4)), dim3(256),
+                       0, s, a);
+  else  // up to 1024 stars: one chain per block (48 KB of LDS)
+    hipLaunchKernelGGL((kinetic_rows_kernel<1, 3072, 5>), dim3((unsigned)n), dim3(64), 0, s, a);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }

@@ -106,20 +106,24 @@ __device__ __forceinline__ double rows_pairwise(const double* a, int64_t n) {
   }
 }
 
-// One wave per chain (4 chains per 256-thread block): lanes over the stars
-// evaluate H once per star, draw p and write the two sums' terms into the
-// wave's LDS rows in NumPy's array layout (p**2 / H and log(abs(H))); lane 0
-// and lane 1 then sum them in NumPy's pairwise order.
-constexpr int kKinMaxD = 768;  // 3 x 256 stars
-
-__global__ void __launch_bounds__(256) kinetic_rows_kernel(KineticArgs a) {
-  __shared__ double terms[4][2][kKinMaxD];
+// One wave per chain (WAVES chains per block): lanes over the stars evaluate
+// H once per star, draw p and write the two sums' terms into the wave's LDS
+// rows in NumPy's array layout (p**2 / H and log(abs(H))); lane 0 and lane 1
+// then sum them in NumPy's pairwise order.  Two shapes: 4 chains of up to 256
+// stars per block (the reversible-jump driver's usual N_max), 1 chain of up
+// to 1024 (rows wider than 768 doubles); DEPTH covers the pairwise halving
+// (128 x 2^DEPTH >= MAXD).  A chain with more stars than MAXD / 3 gets T = NaN.
+template <int WAVES, int MAXD, int DEPTH>
+__global__ void __launch_bounds__(WAVES * 64) kinetic_rows_kernel(KineticArgs a) {
+  __shared__ double terms[WAVES][2][MAXD];
   const int wv = threadIdx.x / 64, lane = threadIdx.x % 64;
-  const int64_t c = (int64_t)blockIdx.x * 4 + wv;
+  const int64_t c = (int64_t)blockIdx.x * WAVES + wv;
   const bool live = c < a.n;
   const double* q = a.q + (live ? c : 0) * a.ld;
   double* p = a.p + (live ? c : 0) * a.ld;
-  const int64_t d = live ? 3 * (int64_t)a.K[c] : 0;
+  const int64_t d0 = live ? 3 * (int64_t)a.K[c] : 0;
+  const bool over = d0 > MAXD;  // wave-uniform
+  const int64_t d = over ? 0 : d0;
   double* t1 = terms[wv][0];
   double* t2 = terms[wv][1];
   for (int64_t i = 3 * lane; i < d; i += 3 * 64) {
@@ -147,13 +151,13 @@ __global__ void __launch_bounds__(256) kinetic_rows_kernel(KineticArgs a) {
     t2[i + 1] = lx;
     t2[i + 2] = lx;
   }
-  if (live && a.z)
+  if (live && a.z && !over)
     for (int64_t i = d + lane; i < a.ld; i += 64) p[i] = 0.;
   __syncthreads();
   if (!live || lane > 1) return;
-  const double s = rows_pairwise<3>(lane == 0 ? t1 : t2, d);
+  const double s = rows_pairwise<DEPTH>(lane == 0 ? t1 : t2, d);
   const double s2 = __shfl_down(s, 1, 64);  // lane 1's sum to lane 0
-  if (lane == 0) a.T[c] = (s + s2) / 2.;
+  if (lane == 0) a.T[c] = over ? __builtin_nan("") : (s + s2) / 2.;
 }
 #pragma clang fp contract(on)
 

@@ -464,7 +464,8 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
     if (cfg->states[c].pos < 0 || cfg->states[c].pos > 624)
       return fail(RHMC_ERR_ARG, "states[c].pos must be in [0, 624]");
   if (cfg->n_iter < 0 || cfg->n_steps < 0) return fail(RHMC_ERR_ARG, "n_iter or n_steps < 0");
-  if (cfg->N_max < 1 || cfg->N_max > 256) return fail(RHMC_ERR_ARG, "N_max must be in [1, 256]");
+  if (cfg->N_max < 1 || cfg->N_max > 1024)
+    return fail(RHMC_ERR_ARG, "N_max must be in [1, 1024]");
   if (cfg->rows < 3 || cfg->cols < 3) return fail(RHMC_ERR_ARG, "rows / cols < 3");
   if ((cfg->n_g_ff2 > 0 && !cfg->schedule_g_ff2) || (cfg->n_beta > 0 && !cfg->schedule_beta) ||
       cfg->n_g_ff2 < 0 || cfg->n_beta < 0)
@@ -825,13 +826,13 @@ struct Plan {
 Plan make_plan(const std::vector<int64_t>& idx, const std::vector<int32_t>& K,
                const std::vector<char>& ragged_ok) {
   Plan pl;
-  std::vector<int64_t> cls[3];
+  std::vector<int64_t> cls[5];  // the register-slot classes of the engine's ragged launches
   std::vector<std::pair<int32_t, std::vector<int64_t>>> groups;
   std::map<int32_t, size_t> where;
   for (int64_t c : idx) {
     const int32_t k = K[c];
     if (ragged_ok[k]) {
-      cls[k <= 64 ? 0 : k <= 128 ? 1 : 2].push_back(c);
+      cls[k <= 64 ? 0 : k <= 128 ? 1 : k <= 256 ? 2 : k <= 512 ? 3 : 4].push_back(c);
       continue;
     }
     auto it = where.find(k);
@@ -844,7 +845,7 @@ Plan make_plan(const std::vector<int64_t>& idx, const std::vector<int32_t>& K,
   }
   for (auto& v : cls) {
     if (v.empty()) continue;
-    int32_t lo = 256, hi = 1;
+    int32_t lo = 1024, hi = 1;
     for (int64_t c : v) {
       lo = std::min(lo, K[c]);
       hi = std::max(hi, K[c]);
@@ -1006,10 +1007,10 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   });
   RJ_HIP(hipMemcpyAsync(w->Q0, w->Zh, (size_t)(n * W) * 8, hipMemcpyHostToDevice, s0));
   RJ_HIP(hipStreamSynchronize(s0));  // Zh is the draws' staging next
-  std::vector<char> ragged_ok(257, 0);
+  std::vector<char> ragged_ok((size_t)cfg->N_max + 1, 0);
   {
     int32_t ok = 0;
-    for (int k = 1; k <= std::min(256, cfg->N_max); ++k) {
+    for (int k = 1; k <= cfg->N_max; ++k) {
       if (int rc = rhmc_ragged_ok(ctx, P0, k, &ok)) return rc;
       ragged_ok[k] = (char)ok;
     }
@@ -1088,8 +1089,16 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       h.E0 = V0[c] + w->T0h[c];
       const int64_t r = l * rec_stride + rec_off + c;
       if (rec) {
-        if (rec_q) std::copy(w->recq + c * W, w->recq + (c + 1) * W, rec->q_chain + r * W);
-        if (rec_p) std::copy(w->recp + c * W, w->recp + (c + 1) * W, rec->p_chain + r * W);
+        // the rows are zero past 3 K on the device: copy the 3 K, write the zeros
+        const int64_t d = 3 * (int64_t)h.K;
+        if (rec_q) {
+          double* dst = rec->q_chain + r * W;
+          std::fill(std::copy(w->recq + c * W, w->recq + c * W + d, dst), dst + W, 0.);
+        }
+        if (rec_p) {
+          double* dst = rec->p_chain + r * W;
+          std::fill(std::copy(w->recp + c * W, w->recp + c * W + d, dst), dst + W, 0.);
+        }
         if (rec->V_chain) rec->V_chain[r] = V0[c];
         if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
         if (rec->E_chain) rec->E_chain[r] = h.E0;

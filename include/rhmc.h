@@ -261,7 +261,7 @@ int rhmc_rows_copy_device(rhmc_ctx* ctx, const double* d_src, int64_t ld_src,
  * d_z + d_zoff[c], p zeroed past 3 K), then T[c] = (sum p^2/H(q) + sum
  * ln|H(q)|) / 2 (:353-363) with NumPy's pairwise summation order.  H
  * follows the reference's operation order (:260-292, g_ff2 / g_xx / B /
- * f_low from P). */
+ * f_low from P).  1 <= d_K[c] <= 1024 (a larger count gets T = NaN). */
 int rhmc_kinetic_rows_device(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q, double* d_p,
                              int64_t ld, const int32_t* d_K, const double* d_z,
                              const int64_t* d_zoff, int64_t n, double* d_T, void* stream);

@@ -145,7 +145,7 @@ typedef struct rhmc_rj_record {
 /*
  * Run n_iter + 1 iterations on n chains.  q: host [n][3 N_max], chain c's
  * first 3 K[c] entries (flux in counts, x, y per star; format_q); K: [n]
- * star counts, 1 <= K[c] <= N_max <= 256.  Both are updated in place to the
+ * star counts, 1 <= K[c] <= N_max <= 1024.  Both are updated in place to the
  * chains' final states.  seeds: [n] (np.random.seed values, < 2^32).
  * P: the engine parameters (g_ff2 / beta replaced per iteration by the
  * schedules; V_prior_const must be set; use_prior selects the prior term of

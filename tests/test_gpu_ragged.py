@@ -165,3 +165,52 @@ def test_rows_copy_and_kinetic(gpu_lib):
         np.testing.assert_allclose(Tg[c], g.T(pw, H), rtol=2e-15, atol=1e-15)
     assert np.array_equal(T2.cpu().numpy(), Tg)
     ctx.close()
+
+
+def test_kinetic_rows_past_256_stars(gpu_lib):
+    """Rows wider than 768 doubles take the one-chain-per-block kinetic kernel
+    (up to 1024 stars, pairwise depth 5): p bit for bit as the host, T to
+    NumPy's last ulp; a chain of more than 1024 stars gets T = NaN."""
+    import torch
+    capi = gpu_lib
+    z = load_golden("traj_bigk")
+    par = R.params_from_npz(z)
+    ctx = capi.Context(z["D"])
+    P = capi_params(capi, par)
+    rs = np.random.RandomState(9)
+    Ks = [300, 1024, 5, 777, 257]
+    ld = 3 * 1024
+    q = np.zeros((len(Ks), ld))
+    for c, K in enumerate(Ks):
+        q[c, 0:3 * K:3] = par["f_lim"] * np.exp(1 + 2 * rs.rand(K))
+        q[c, 1:3 * K:3] = 1 + 30 * rs.rand(K)
+        q[c, 2:3 * K:3] = 1 + 30 * rs.rand(K)
+    dev = torch.device("cuda:0")
+    qd = torch.from_numpy(q).to(dev)
+    zoff = np.concatenate([[0], np.cumsum([3 * K for K in Ks])[:-1]]).astype(np.int64)
+    zz = rs.randn(sum(3 * K for K in Ks))
+    pd = torch.full((len(Ks), ld), 7.0, dtype=torch.float64, device=dev)
+    Td = torch.zeros(len(Ks), dtype=torch.float64, device=dev)
+    Kd = torch.tensor(Ks, dtype=torch.int32, device=dev)
+    zd, zoffd = torch.from_numpy(zz).to(dev), torch.from_numpy(zoff).to(dev)
+    ctx.kinetic_rows_device(P, qd.data_ptr(), pd.data_ptr(), ld, Kd.data_ptr(), zd.data_ptr(),
+                            zoffd.data_ptr(), len(Ks), Td.data_ptr())
+    torch.cuda.synchronize()
+    from rhmc_amd import sampler
+    g = sampler.multi_gym(dt=par["dt"], g_xx=par["g_xx"], g_ff=par["g_ff"], g_ff2=par["g_ff2"])
+    pg, Tg = pd.cpu().numpy(), Td.cpu().numpy()
+    for c, K in enumerate(Ks):
+        H = g._H_vec(q[c, :3 * K])
+        pw = zz[zoff[c]:zoff[c] + 3 * K] * np.sqrt(H)
+        assert np.array_equal(pg[c, :3 * K], pw), c
+        assert not pg[c, 3 * K:].any()
+        np.testing.assert_allclose(Tg[c], g.T(pw, H), rtol=2e-15, atol=1e-15)
+    Kbig = torch.tensor([1025], dtype=torch.int32, device=dev)
+    qb = torch.zeros((1, 3 * 1025), dtype=torch.float64, device=dev)
+    pb = torch.zeros_like(qb)
+    Tb = torch.zeros(1, dtype=torch.float64, device=dev)
+    ctx.kinetic_rows_device(P, qb.data_ptr(), pb.data_ptr(), 3 * 1025, Kbig.data_ptr(), 0, 0, 1,
+                            Tb.data_ptr())
+    torch.cuda.synchronize()
+    assert np.isnan(Tb.cpu().numpy()[0])
+    ctx.close()

@@ -137,6 +137,53 @@ def test_native_two_pipes_equal_one(gpu_lib):
         np.testing.assert_allclose(x, y, rtol=1e-12, atol=1e-12)
 
 
+def test_native_across_256_stars(gpu_lib):
+    """Reversible jumps around 256 stars (N_max 300, a 64x64 image of 300
+    reference stars, hugek.npz): chains of 255-257 stars, so the phases mix
+    the engine's 4-slot LDS-table launches with its 8-slot global-table ones
+    and a birth / death / split / merge proposal moves a chain between them;
+    the momentum draw and T run the one-chain-per-block kinetic kernel (rows
+    of 900 doubles).  The native driver equals the NumPy loop on the same
+    engine."""
+    z = load_golden("hugek")
+    name = "h300"
+    par = R.params_from_npz(z, name + "/par_")
+
+    def make():
+        g = _gym(par)
+        g.D = z[name + "/D"]
+        return g
+    q = z[name + "/q"][0]
+    g0 = make()
+    stars = np.stack([g0.flux2mag_converter(q[0::3]), q[1::3], q[2::3]], 1)
+    rs = np.random.RandomState(17)
+    starts = []
+    for c in range(12):
+        m = stars[rs.permutation(300)[:255 + c % 3]].copy()
+        m[:, 1:] += rs.uniform(-0.2, 0.2, (len(m), 2))
+        starts.append(m)
+    seeds = list(range(900, 912))
+    kw = dict(f_pos=False, delta=1e-6, Niter=5, Nsteps=3, dt=0.05, N_max=300,
+              P_move=[0.2, 0.4, 0.4])
+    ok = _completing(make, starts, seeds, kw)
+    assert len(ok) >= 6
+    a, b = make(), make()
+    qa = a.run_RHMC_rj_batched([m.copy() for m, _ in ok], [s for _, s in ok], engine="native",
+                               **kw)
+    qb = b.run_RHMC_rj_batched([m.copy() for m, _ in ok], [s for _, s in ok], engine="python",
+                               **kw)
+    np.testing.assert_array_equal(a.move_chain, b.move_chain)
+    np.testing.assert_array_equal(a.N_chain, b.N_chain)
+    np.testing.assert_array_equal(a.A_chain, b.A_chain)
+    assert_state_close(a.q_chain, b.q_chain, 1e-11, "q_chain")
+    np.testing.assert_allclose(a.E_chain, b.E_chain, rtol=1e-12)
+    for x, y in zip(qa, qb):
+        assert x.size == y.size
+        np.testing.assert_allclose(x, y, rtol=1e-11, atol=1e-11)
+    assert a.N_chain[0].min() <= 256 < a.N_chain[0].max()      # both slot classes from the start
+    assert (a.move_chain > 0).any()
+
+
 def test_native_record_buffers_reused_only_when_unreferenced(gpu_lib):
     """A second run writes its q_chain / p_chain records into the first run's
     memory only when nothing but the sampler holds it; the records equal a
