@@ -56,5 +56,5 @@ def test_energy_device_errors(gpu_lib):
     with pytest.raises(capi.RhmcError, match="q is NULL"):
         ctx.energy_device(P, 0, 0, 0, 0, 4, 1)
     with pytest.raises(capi.RhmcError, match="K must be"):
-        ctx.energy_device(P, 1, 0, 0, 0, 4, 300)
+        ctx.energy_device(P, 1, 0, 0, 0, 4, 1025)
     ctx.close()

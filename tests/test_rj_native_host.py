@@ -177,7 +177,7 @@ def test_argument_errors(rj):
     with pytest.raises(capi.RhmcError, match="P_move"):
         rj.run(P, q, [1], **dict(base, P_move=[0.5, 0.2, 0.2]), physics=phys)
     with pytest.raises(capi.RhmcError, match="N_max"):
-        rj.run(P, q, [1], **dict(base, N_max=300), physics=phys)
+        rj.run(P, q, [1], **dict(base, N_max=1025), physics=phys)
     with pytest.raises(capi.RhmcError, match="fmin"):
         rj.run(P, q, [1], **dict(base, fmin=0.), physics=phys)
     with pytest.raises(ValueError):
