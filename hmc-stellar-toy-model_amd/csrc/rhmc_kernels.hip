@@ -613,6 +613,8 @@ struct EnergyArgs {
 };
 
 // V (sampler_RHMC.py:294-351) and T at H(q) (:353-363), one wave per chain.
+// Ragged sets (a.Kc): the chain's row and star count; the wave's table region
+// is sized by the set's largest K (a.K), laid out by the chain's.
 template <int MAXK>
 __global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
   extern __shared__ double lds[];
@@ -622,10 +624,13 @@ __global__ void __launch_bounds__(256) energy_kernel(EnergyArgs a) {
   const int64_t chain = stage_image(lds, a.D, g.npix, W);
   if (chain >= a.n_chains) return;
   const int lane = lane_id();
-  const int K = a.K;
-  const Tables tab = carve_tables(lds + g.npix + (threadIdx.x / kWave) * table_doubles(K, g.rows, g.cols), K, g);
+  int64_t row, ld;
+  int K;
+  chain_row(a, chain, row, K, ld);
+  const Tables tab = carve_tables(
+      lds + g.npix + (threadIdx.x / kWave) * table_doubles(a.K, g.rows, g.cols), K, g);
   const bool owner = lane < K;
-  const int64_t base = chain * 3 * (int64_t)K + 3 * (owner ? lane : 0);
+  const int64_t base = row * ld + 3 * (owner ? lane : 0);
   const double f = a.q[base], x = a.q[base + 1], y = a.q[base + 2];
 
   if (a.T) {
@@ -1614,7 +1619,7 @@ bool use_pixk(const rhmc_ctx* ctx, int K, const Consts& c) {
          (ctx->rows == 32 || ctx->rows == 48);
 }
 
-template <int IMG, int SOLVER = RHMC_SOLVER_IMPLICIT>
+template <int IMG, int SOLVER = RHMC_SOLVER_IMPLICIT, bool RAGGED = false>
 int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s, int f_pos = 0) {
   using PK = PixK<IMG, 10>;  // LDS layout does not depend on the columns per pass
   int W = 4;
@@ -1624,7 +1629,7 @@ int launch_pk(const rhmc_ctx* ctx, LeapArgsKR a, hipStream_t s, int f_pos = 0) {
   a.Df = ctx->d_Df;
   const int64_t waves = (a.n_chains + PK::CPW - 1) / PK::CPW;
   const dim3 grid((unsigned)((waves + W - 1) / W)), block(W * kWave);
-  hipLaunchKernelGGL((leapfrog_pk<IMG, 10, SOLVER>), grid, block, lds, s, a, f_pos);
+  hipLaunchKernelGGL((leapfrog_pk<IMG, 10, SOLVER, RAGGED>), grid, block, lds, s, a, f_pos);
   HIP_TRY(hipGetLastError());
   return RHMC_OK;
 }
@@ -1748,14 +1753,17 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
 // reversible-jump driver).  Which star counts the automatic dispatch serves
 // with a slotted one-wave-per-chain kernel — for both the step and the
 // energy — where chains of different K can share a launch: 1 = the dense
-// kernel (32/48-px images, from 11 stars), 2 = the windowed kernel; 0 = a
-// kernel with a fixed K per launch (one-star, pixel-major, multi-star
-// register-window, the LDS-image generic kernels).
+// kernel (32/48-px images, from 11 stars), 2 = the windowed kernel, 3 = the
+// pixel-major kernel (2-10 stars on 32/48-px fp32-exact images) with the
+// LDS-image energy kernel; 0 = a kernel with a fixed K per launch (one-star,
+// multi-star register-window).
 int ragged_family(const rhmc_ctx* ctx, const Consts& c, int K) {
   if (K < 1 || K > kMaxK) return 0;
   if (dense_path(ctx, K, c)) return 1;
   if (K == 1) return 0;
-  if (use_pixk(ctx, K, c) || use_tiledrk(ctx, K, c)) return 0;
+  if (use_pixk(ctx, K, c))  // the energy of those K: the LDS-image kernel
+    return !use_windowed(ctx, K) ? 3 : 0;
+  if (use_tiledrk(ctx, K, c)) return 0;
   return use_windowed(ctx, K) && window_exact(c) ? 2 : 0;
 }
 
@@ -1791,6 +1799,28 @@ int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, dou
   if ((rc = ragged_check(ctx, a.c, K_min, K_max, ld, &fam))) return rc;
   if (n == 0) return RHMC_OK;
   HIP_TRY(hipSetDevice(ctx->device));
+  if (fam == 3) {  // the pixel-major kernel, each chain its own row and K
+    LeapArgsKR t;
+    t.q = d_q;
+    t.p = d_p;
+    t.fp_iters = nullptr;
+    t.status = nullptr;
+    t.D = ctx->d_D;
+    t.Df = nullptr;
+    t.n_chains = n;
+    t.K = K_max;
+    t.n_steps = n_steps;
+    t.side = ctx->rows;
+    t.pad = 0;
+    t.c = a.c;
+    t.dtv = nullptr;
+    t.steps = nullptr;
+    t.Kc = d_K;
+    t.rows = d_rows;
+    t.ld = ld;
+    return ctx->rows == 32 ? launch_pk<32, RHMC_SOLVER_IMPLICIT, true>(ctx, t, s)
+                           : launch_pk<48, RHMC_SOLVER_IMPLICIT, true>(ctx, t, s);
+  }
   const int path = dense_path(ctx, K_max, a.c);
   a.g = make_geometry(ctx->rows, ctx->cols);
   a.q = d_q;
@@ -1831,6 +1861,23 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   const int path = dense_path(ctx, K_max, a.c);
   size_t lds;
   int W;
+  if (fam == 3) {  // the LDS-image kernel, each chain its own row and K
+    if ((rc = pick_waves(ctx, K_max, &lds, &W))) return rc;
+    a.q = d_q;
+    a.p = nullptr;
+    a.V = d_V;
+    a.T = nullptr;
+    a.D = ctx->d_D;
+    a.n_chains = n;
+    a.K = K_max;
+    a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
+    a.g = make_geometry(ctx->rows, ctx->cols);
+    a.Kc = d_K;
+    a.rows = d_rows;
+    a.ld = ld;
+    const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
+    return dispatch_k<EnergyLaunch>(K_max, grid, block, lds, s, a);
+  }
   if (path || K_max > kMaxKLds) {
     if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
   } else {  // potential-only windowed tables, as launch_energy

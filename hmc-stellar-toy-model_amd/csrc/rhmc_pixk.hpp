@@ -337,7 +337,7 @@ struct PixK {
       gx = -fma(kCtr - st.x, s0, s1) * lc.inv_var;          // :405
       gy = -fma(kCtr - st.y, s0, s2) * lc.inv_var;          // :406
     }
-#else
+#else  // (K wave-uniform here: not for ragged sets, whose two chains may differ)
     gf = gx = gy = 0.0;
 #pragma unroll
     for (int k = 0; k < KMAX; ++k) {
@@ -359,8 +359,13 @@ struct PixK {
 
 // Two chains per wave, W waves per workgroup, one star per lane (K <= KMAX).
 // SOLVER as in leapfrog_kr: RHMC_single_step, an explicit integrator (f_pos =
-// the flux wall) or kSolverHmcRandom.
-template <int IMG, int KMAX, int SOLVER = RHMC_SOLVER_IMPLICIT>
+// the flux wall) or kSolverHmcRandom.  Ragged sets (a.Kc): each chain's own
+// row and star count; the two chains of a wave may differ in K — everything
+// that depends on it is per lane (a chain's lanes), and the pixel passes run
+// all KMAX slots with zero tables for the stars a chain lacks — so a chain's
+// results are those of a fixed-K launch on it.  RAGGED is a separate
+// instantiation, so the fixed-K kernel keeps its wave-uniform K.
+template <int IMG, int KMAX, int SOLVER = RHMC_SOLVER_IMPLICIT, bool RAGGED = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_pk(LeapArgsKR a, int f_pos) {
   // (HMC_random ran two columns per pass until the unguarded accumulation
@@ -382,13 +387,19 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   const int64_t chain = PK::CPW * wave + h;
   const bool real = chain < a.n_chains;  // ragged tail: mirror the wave's first chain
   const int64_t chain_r = real ? chain : PK::CPW * wave;
-  const int64_t cbase = chain_r * 3 * (int64_t)a.K;
+  int64_t row = chain_r, ldq = 3 * (int64_t)a.K;
+  int K = a.K;
+  if constexpr (RAGGED) {  // a ragged set: this chain's row and star count
+    row = a.rows ? a.rows[chain_r] : chain_r;
+    K = a.Kc[row];
+    ldq = a.ld;
+  }
+  const int64_t cbase = row * ldq;
   const int slot = (threadIdx.x / kWave) * PK::CPW + h;
   KRStar* tab = reinterpret_cast<KRStar*>(lds + kExpTab) + slot * PK::NSTAR;
   double* rtab = lds + kExpTab + PK::star_doubles(W) + (size_t)slot * PK::tab_doubles();
   const Consts& c = a.c;
   const LeanConsts lc = lean_consts(c);
-  const int K = a.K;
   double f[1], x[1], y[1], pf[1], px[1], py[1];
   bool own[1];
   own[0] = m < K;
@@ -425,7 +436,9 @@ leapfrog_pk(LeapArgsKR a, int f_pos) {
   int lid;
   asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(lid));
   const int64_t chain_o = PK::CPW * wave + lid / PK::LPC;
-  const int64_t e_o = (chain_o < a.n_chains ? chain_o : PK::CPW * wave) * 3 * (int64_t)a.K +
+  const int64_t chain_or = chain_o < a.n_chains ? chain_o : PK::CPW * wave;
+  const int64_t e_o = (RAGGED ? (a.rows ? a.rows[chain_or] : chain_or) * a.ld
+                             : chain_or * 3 * (int64_t)a.K) +
                       3 * (int64_t)(own[0] ? lid % PK::LPC : 0);
   unsigned nf = 0u;
   if (own[0] && real) {

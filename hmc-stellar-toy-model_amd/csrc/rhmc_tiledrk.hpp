@@ -50,6 +50,12 @@ struct LeapArgsKR {
   Consts c;
   const double* dtv;      // kSolverHmcRandom: per-coordinate steps [3K]
   const int32_t* steps;   // kSolverHmcRandom: trajectory length per chain
+  // ragged sets (rhmc_leapfrog_ragged_device; the pixel-major kernel's implicit
+  // step only): chain i is row rows[i] (null: i) of [*][ld] arrays with Kc[row]
+  // stars; K is then the set's largest star count
+  const int32_t* Kc = nullptr;
+  const int64_t* rows = nullptr;
+  int64_t ld = 0;
 };
 
 // leapfrog_kr's SOLVER for samplers.HMC_random trajectories (not a C-ABI

@@ -826,13 +826,16 @@ struct Plan {
 Plan make_plan(const std::vector<int64_t>& idx, const std::vector<int32_t>& K,
                const std::vector<char>& ragged_ok) {
   Plan pl;
-  std::vector<int64_t> cls[5];  // the register-slot classes of the engine's ragged launches
+  // the engine's ragged launch classes: one kernel family and one register-slot
+  // count each (2-10 stars: the pixel-major kernel on 32/48-px images; then the
+  // slot counts of the dense / windowed kernels)
+  std::vector<int64_t> cls[6];
   std::vector<std::pair<int32_t, std::vector<int64_t>>> groups;
   std::map<int32_t, size_t> where;
   for (int64_t c : idx) {
     const int32_t k = K[c];
     if (ragged_ok[k]) {
-      cls[k <= 64 ? 0 : k <= 128 ? 1 : k <= 256 ? 2 : k <= 512 ? 3 : 4].push_back(c);
+      cls[k <= 10 ? 0 : k <= 64 ? 1 : k <= 128 ? 2 : k <= 256 ? 3 : k <= 512 ? 4 : 5].push_back(c);
       continue;
     }
     auto it = where.find(k);

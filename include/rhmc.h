@@ -233,7 +233,9 @@ int rhmc_leapfrog_device(rhmc_ctx* ctx, const rhmc_params* P, double* d_q,
  * stars (its first 3 K entries; d_K indexed by row).  One launch serves every
  * star count in [K_min, K_max] when the automatic dispatch runs a slotted
  * one-wave-per-chain kernel for each of them — the dense kernel on 32/48-px
- * images from 11 stars, the windowed kernel (rhmc_ragged_ok says which K);
+ * images from 11 stars, the windowed kernel — or the pixel-major kernel (2-10
+ * stars on 32/48-px images whose pixels are exact in fp32; a launch takes one
+ * family: 2-10 and 11+ stars are separate sets) (rhmc_ragged_ok says which K);
  * K_min and K_max must need the same register slots (1-64, 65-128, 129-256,
  * 257-512, 513-1024 stars), else RHMC_ERR_ARG, and a K the slotted kernels do not serve gives
  * RHMC_ERR_UNSUPPORTED.  Each chain's results equal those of a fixed-K call

@@ -3,10 +3,10 @@ device-resident reversible-jump driver runs on: chains of different star
 counts in one launch, as rows of padded device arrays.
 
 * rhmc_leapfrog_ragged_device / rhmc_energy_ragged_device equal fixed-K
-  calls on the same chains bit for bit (the slotted kernels are
-  batch-invariant; a row list in any order, chains of 11..64 stars on the
-  dense kernel of a 32-px image, 65..90 on the windowed kernel of a 256-px
-  image);
+  calls on the same chains bit for bit (the kernels are batch-invariant; a
+  row list in any order, chains of 11..64 stars on the dense kernel of a
+  32-px image, 65..90 on the windowed kernel of a 256-px image, 2..10 on the
+  pixel-major kernel of a 32-px image, two chains of different K per wave);
 * rhmc_ragged_ok names the star counts the slotted kernels serve;
 * rhmc_rows_copy_device gathers / scatters rows;
 * rhmc_kinetic_rows_device draws p = z sqrt(H(q)) bit for bit as the host
@@ -39,7 +39,7 @@ def _set(par, Ks, n_pix, rs, ld):
     return q, p
 
 
-@pytest.mark.parametrize("case", ["dense32", "win256"])
+@pytest.mark.parametrize("case", ["dense32", "win256", "pixk32"])
 def test_ragged_equals_fixed_K(gpu_lib, case):
     import torch
     capi = gpu_lib
@@ -47,6 +47,10 @@ def test_ragged_equals_fixed_K(gpu_lib, case):
         z = load_golden("traj_bigk")
         D, par = z["D"], R.params_from_npz(z)
         Ks = [11, 30, 17, 64, 11, 45, 30, 23, 64, 12, 50, 11, 33]
+    elif case == "pixk32":
+        z = load_golden("traj_bigk")
+        D, par = z["D"], R.params_from_npz(z)
+        Ks = [2, 7, 10, 3, 3, 9, 5, 10, 2, 6, 8, 4, 7, 5, 9]
     else:
         z = load_golden("traj_bigk256")
         D, par = z["D"], R.params_from_npz(z)
@@ -92,7 +96,7 @@ def test_ragged_ok_and_argument_checks(gpu_lib):
     ctx = capi.Context(z["D"])                      # 32 px: dense from 11 stars
     P = capi_params(capi, par)
     assert [ctx.ragged_ok(P, K) for K in (1, 2, 10, 11, 64, 65, 256)] == \
-        [False, False, False, True, True, True, True]
+        [False, True, True, True, True, True, True]   # 2-10: the pixel-major kernel
     dev = torch.device("cuda:0")
     q = torch.zeros((2, 3 * 70), dtype=torch.float64, device=dev)
     K = torch.tensor([60, 70], dtype=torch.int32, device=dev)
@@ -100,9 +104,13 @@ def test_ragged_ok_and_argument_checks(gpu_lib):
         ctx.leapfrog_ragged_device(P, q.data_ptr(), q.data_ptr(), 210, 0, K.data_ptr(), 2, 60,
                                    70, 1)
     assert e.value.code == capi.RHMC_ERR_ARG
-    with pytest.raises(capi.RhmcError) as e:          # 5 stars: the pixel-major kernel
+    with pytest.raises(capi.RhmcError) as e:          # 5 and 20 stars: two kernel families
         ctx.leapfrog_ragged_device(P, q.data_ptr(), q.data_ptr(), 210, 0, K.data_ptr(), 2, 5,
                                    20, 1)
+    assert e.value.code == capi.RHMC_ERR_UNSUPPORTED
+    with pytest.raises(capi.RhmcError) as e:          # 1 star: the one-star kernels
+        ctx.leapfrog_ragged_device(P, q.data_ptr(), q.data_ptr(), 210, 0, K.data_ptr(), 2, 1,
+                                   5, 1)
     assert e.value.code == capi.RHMC_ERR_UNSUPPORTED
     with pytest.raises(capi.RhmcError):               # ld too small for K_max
         ctx.leapfrog_ragged_device(P, q.data_ptr(), q.data_ptr(), 30, 0, K.data_ptr(), 2, 11,
