@@ -353,6 +353,9 @@ def bench_rj(args, wl, gpu, world, rank):
                   P_move=[0.6, 0.2, 0.2])
         name, K0, D = wl.name, wl.K, wl.D
     g.device = gpu
+    # every chain starts with K0 stars: one [n, K0, 3] array (run_RHMC_rj_batched
+    # packs it in one native pass)
+    starts = np.stack(starts)
     seeds = [1000 * rank + c for c in range(n_chains)]
     for _ in range(args.warmup):
         g.run_RHMC_rj_batched(starts, seeds, n_pipes=args.rj_pipes, **kw)

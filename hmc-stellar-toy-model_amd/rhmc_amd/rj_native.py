@@ -138,12 +138,24 @@ def beta_eval(a, b, x):
 
 def pack_starts(q_models, N_max, flux_to_count=0.):
     """Chain starts -> (q [n][3 N_max] zero-padded, K [n]) in one native pass.
-    q_models: [K_c, 3] arrays — (mag, x, y) rows converted by format_q's
-    mag2flux (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 —
-    or flat flux-count vectors with flux_to_count = 0."""
+    q_models: [K_c, 3] arrays, or one [n, K, 3] array when every chain has K
+    stars — (mag, x, y) rows converted by format_q's mag2flux
+    (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 — or flat
+    flux-count vectors with flux_to_count = 0."""
     n = len(q_models)
     if n == 0:
         return np.zeros((0, 3 * int(N_max))), np.zeros(0, np.int32)
+    if isinstance(q_models, np.ndarray) and q_models.ndim == 3:   # [n, K, 3]: one K
+        if q_models.shape[2] != 3:
+            raise ValueError("starts [n, K, 3] hold (mag, x, y) rows")
+        K = np.full(n, q_models.shape[1], np.int32)
+        if K[0] < 1 or K[0] > N_max:
+            raise ValueError("every start needs 1 .. N_max stars")
+        rows = np.ascontiguousarray(q_models, dtype=np.float64).reshape(-1)
+        q = np.empty((n, 3 * int(N_max)))
+        _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
+                                        float(flux_to_count), q.ctypes.data))
+        return q, K
     flat = [np.asarray(m, dtype=np.float64) for m in q_models]
     if all(m.ndim == 2 and m.shape[1] == 3 for m in flat):      # [K, 3] rows
         K = np.fromiter((len(m) for m in flat), dtype=np.int32, count=n)

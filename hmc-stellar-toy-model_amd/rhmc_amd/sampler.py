@@ -697,7 +697,9 @@ class multi_gym(base_class):
         (chains grouped by K, so the kernels see ordinary fixed-K batches).
 
         q_models_0: a list of [K_c, 3] (mag, x, y) arrays, or of the flat
-        flux-count q vectors a run returned (taken as they are: a resume).
+        flux-count q vectors a run returned (taken as they are: a resume); or
+        one [n, K, 3] array when every chain starts with K stars (packed in one
+        pass, without a Python object per chain).
         Returns a list of the chains' final q; sets q_chain / p_chain [Niter+1, n, 3 N_max],
         E/V/T_chain, A_chain, move_chain, N_chain [Niter+1, n] (iteration-major,
         like run_RHMC_batched).
@@ -862,8 +864,14 @@ class multi_gym(base_class):
             assert False                                  # :1205-1207 (prior required)
         # the starts in one native pass: [K, 3] (mag, x, y) rows through format_q's
         # mag2flux (bit-identical to _start_q), flat q vectors (a resume) as they are
-        dims = {np.ndim(m) for m in q_models_0}
-        if dims <= {2}:
+        if isinstance(q_models_0, np.ndarray) and q_models_0.ndim == 3:
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count)
+            dims = None
+        else:
+            dims = {np.ndim(m) for m in q_models_0}
+        if dims is None:
+            pass
+        elif dims <= {2}:
             packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count)
         elif dims <= {1}:
             packed = rj_native.pack_starts(q_models_0, N_max)

@@ -170,3 +170,21 @@ def test_native_start_packing_is_format_q():
     assert np.array_equal(q2, q) and np.array_equal(K2, K)
     with pytest.raises(ValueError):
         rj_native.pack_starts([np.ones((2, 3))], 1)
+
+
+def test_native_start_packing_array_form():
+    """One [n, K, 3] start array packs as the list of its rows does (the
+    multi-threaded native pass over 4,096 chains included)."""
+    from rhmc_amd import rj_native, sampler
+    g = sampler.multi_gym(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.)
+    rs = np.random.RandomState(13)
+    arr = np.stack([15 + 8.3 * rs.rand(4096, 51), 32 * rs.rand(4096, 51),
+                    32 * rs.rand(4096, 51)], 2)
+    q, K = rj_native.pack_starts(arr, 122, g.flux_to_count)
+    q2, K2 = rj_native.pack_starts(list(arr), 122, g.flux_to_count)
+    assert np.array_equal(q, q2) and np.array_equal(K, K2) and (K == 51).all()
+    assert np.array_equal(q[7, :153], g.format_q(arr[7].copy()))
+    with pytest.raises(ValueError):
+        rj_native.pack_starts(arr, 50, g.flux_to_count)
+    with pytest.raises(ValueError):
+        rj_native.pack_starts(np.ones((2, 3, 2)), 10)
