@@ -2654,7 +2654,7 @@ int rhmc_kinetic_rows_device(rhmc_ctx* ctx, const rhmc_params* P, const double* 
                              const int64_t* d_zoff, int64_t n, double* d_T, void* stream) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   if (!P) return fail(RHMC_ERR_ARG, "params is NULL");
-  if (n < 0 || ld < 3) return fail(RHMC_ERR_ARG, "kinetic: bad n or ld");
+  if (n < 0 || ld < 3 || n > INT32_MAX) return fail(RHMC_ERR_ARG, "kinetic: bad n or ld");
   if (n == 0) return RHMC_OK;
   if (!d_q || !d_p || !d_K || !d_T || (d_z && !d_zoff))
     return fail(RHMC_ERR_ARG, "kinetic: q, p, K, T (or zoff with z) is NULL");

@@ -1303,9 +1303,12 @@ int pipes_for(const rhmc_rj_config* cfg, int64_t n) {
   // default for the device-resident driver, measured at big-sim4 geometry
   // (profiles/r05_pipes/, three repeats on one box, chain-steps/s): 4,096
   // chains 1.70e7 / 1.82e7 / 1.84e7 with 2 / 3 / 4 pipes; 16,384 chains
-  // 1.80e7 / 2.06e7 / 2.12e7; the flagship (K from 5) 0.99e7 / 1.09e7 / 1.05e7
+  // 1.80e7 / 2.06e7 / 2.12e7.  After the ragged pixel-major launches
+  // (profiles/r05_pipes2/, r05_pipes3/, four repeats): 4,096 chains B4 2.62e7 /
+  // 2.72e7 with 3 / 4 pipes, the flagship 2.64e7 / 2.78e7; 6 and 8 pipes
+  // (more streams than the box's 4 hardware queues) 0.75-0.95x
   int pipes = cfg->n_pipes > 0 ? cfg->n_pipes
-                               : (n >= 16384 ? 4 : n >= 2048 ? 3 : n >= 1024 ? 2 : 1);
+                               : (n >= 4096 ? 4 : n >= 2048 ? 3 : n >= 1024 ? 2 : 1);
   return (int)std::max<int64_t>(1, std::min<int64_t>(pipes, n));
 }
 

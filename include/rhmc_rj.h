@@ -99,7 +99,7 @@ typedef struct rhmc_rj_config {
   int32_t n_pipes;       /* 1: one pass over all chains per phase; 2..4: the chains in
                             that many contiguous parts on as many host threads, so
                             one part's host work overlaps the others' GPU work; 0:
-                            2 from 1,024 chains, 3 from 2,048, 4 from 16,384         */
+                            2 from 1,024 chains, 3 from 2,048, 4 from 4,096          */
   int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
                             seeds[c] (a checkpoint of an earlier run, or any
                             RandomState's get_state(): continue its stream)        */
