@@ -24,6 +24,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <string>
 
 #include "rhmc.h"
@@ -1066,6 +1067,15 @@ int window_unsupported() {
 constexpr int kMaxKGeneric = 16;   // register accumulators of the LDS-image kernels
 constexpr int kMaxKLds = 256;      // slotted kernels, LDS tables: 64 lanes x 4 star slots
 constexpr int kMaxK = 1024;        // slotted kernels, global tables (WinGG): 8 / 16 slots
+// The windowed path's first star count on the global-table policy (WinGG)
+// instead of LDS tables (WinG, whose 2 K 33 doubles per wave cap a CU at one
+// or two waves past 64 stars)
+#ifndef RHMC_WINGG_FROM
+#define RHMC_WINGG_FROM 65
+#endif
+constexpr int kWinGlobalFromK = RHMC_WINGG_FROM;
+static_assert(kWinGlobalFromK == 65 || kWinGlobalFromK == 129 || kWinGlobalFromK == 257,
+              "a register-slot boundary");
 
 // Star slots per lane of the windowed kernels for K stars.
 int win_slots(int K) {
@@ -1078,15 +1088,16 @@ int win_slots(int K) {
 struct WorkTables {
   void* p = nullptr;
   hipStream_t s = nullptr;
-  int get(int K, int64_t n, hipStream_t st, double** out) {
+  // path: the launch's gradient path (0 = windowed); tables only for WinGG
+  int get(int path, int K, int64_t n, hipStream_t st, double** out) {
     *out = nullptr;
-    if (K <= kMaxKLds || n <= 0) return RHMC_OK;
+    if (path != 0 || K < kWinGlobalFromK || n <= 0) return RHMC_OK;
     s = st;
     const size_t bytes = (size_t)n * WinGG::work_doubles(K) * sizeof(double);
     if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
       p = nullptr;
       return fail(RHMC_ERR_NOMEM, "hipMallocAsync of " + std::to_string(bytes) +
-                                      " B of factor tables (K > 256) failed");
+                                      " B of windowed factor tables failed");
     }
     *out = (double*)p;
     return RHMC_OK;
@@ -1125,26 +1136,44 @@ int with_slots(int K, F&& f) {
     default: return f(TypeTag<G>{}, IntTag<4>{});
   }
 }
-// K > 256: the global-table policy at 8 or 16 slots (the only policy
-// instantiated there)
+// K >= kWinGlobalFromK on the windowed path: the global-table policy (the
+// only policy instantiated past 256 stars, 8 or 16 slots)
 template <class F>
 int with_big(int K, F&& f) {
+  if constexpr (kWinGlobalFromK <= 64 * 2)
+    if (K <= 128) return f(TypeTag<WinGG>{}, IntTag<2>{});
+  if constexpr (kWinGlobalFromK <= 64 * 4)
+    if (K <= 256) return f(TypeTag<WinGG>{}, IntTag<4>{});
   if (K <= 512) return f(TypeTag<WinGG>{}, IntTag<8>{});
   return f(TypeTag<WinGG>{}, IntTag<16>{});
 }
+// LDS-table policies below kWinGlobalFromK (windowed) / 256 (dense)
+template <class G, class F>
+int with_slots_lds(int K, F&& f) {
+  if (K <= 64) return f(TypeTag<G>{}, IntTag<1>{});
+  if constexpr (kWinGlobalFromK > 65 || !std::is_same<G, WinG>::value)
+    if (K <= 128) return f(TypeTag<G>{}, IntTag<2>{});
+  if constexpr (kWinGlobalFromK > 129 || !std::is_same<G, WinG>::value)
+    return f(TypeTag<G>{}, IntTag<4>{});
+  return fail(RHMC_ERR_ARG, "no LDS-table slotted kernel for K = " + std::to_string(K));
+}
 template <class F>
 int with_path(int path, int K, F&& f) {
-  if (K > kMaxKLds) return with_big(K, f);
-  if (path == 32) return with_slots<DenseG<32>>(K, f);
+  if (path == 32) return with_slots<DenseG<32>>(K, f);  // dense_path: K <= 256
   if (path == 48) return with_slots<DenseG<48>>(K, f);
-  return with_slots<WinG>(K, f);
+  if (K >= kWinGlobalFromK) return with_big(K, f);
+  return with_slots_lds<WinG>(K, f);
 }
-// The windowed energy kernel's policy: column tables only (WinEG) up to 256
-// stars, the global tables above
+// The windowed energy kernel's policy: column tables only (WinEG) below
+// kWinGlobalFromK, the global tables from there
 template <class F>
 int with_energy_win(int K, F&& f) {
-  if (K > kMaxKLds) return with_big(K, f);
-  return with_slots<WinEG>(K, f);
+  if (K >= kWinGlobalFromK) return with_big(K, f);
+  if (K <= 64) return f(TypeTag<WinEG>{}, IntTag<1>{});
+  if constexpr (kWinGlobalFromK > 65)
+    if (K <= 128) return f(TypeTag<WinEG>{}, IntTag<2>{});
+  if constexpr (kWinGlobalFromK > 129) return f(TypeTag<WinEG>{}, IntTag<4>{});
+  return fail(RHMC_ERR_ARG, "no LDS-table energy kernel for K = " + std::to_string(K));
 }
 
 // Which kernel family serves (K, image): the LDS-image kernels need D and the
@@ -1160,7 +1189,7 @@ bool use_windowed(const rhmc_ctx* ctx, int K) {
 // for one wave, within gfx950's 160 KB; a device with less LDS gets
 // RHMC_ERR_UNSUPPORTED here, not a failed launch).
 int pick_waves_win(const rhmc_ctx* ctx, int K, size_t* lds, int* W) {
-  if (K > kMaxKLds) {  // WinGG: the exp table only
+  if (K >= kWinGlobalFromK) {  // WinGG: the exp table only
     *W = 4;
     *lds = WinGG::lds_bytes(4, K);
     return RHMC_OK;
@@ -1491,7 +1520,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   const int path = dense_path(ctx, K, c);
   const bool win = path || use_windowed(ctx, K);
   if (win && !path && !window_exact(c)) return window_unsupported();
-  if (win && !path && K > kMaxKLds) {  // global tables (WinGG)
+  if (win && !path && K >= kWinGlobalFromK) {  // global tables (WinGG)
     if ((rc = pick_waves_win(ctx, K, &lds, &W))) return rc;
   } else if (win && !path) {  // potential-only windowed tables (WinEG)
     W = 4;
@@ -1514,7 +1543,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
   a.g = make_geometry(ctx->rows, ctx->cols);
   WorkTables wt;
-  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
     auto go = [&](auto gt, auto st) {
@@ -1722,7 +1751,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.n_steps = n_steps;
     if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
     WorkTables wt;
-    if ((rc = wt.get(K, n_chains, s, &a.g.work))) return rc;
+    if ((rc = wt.get(path, K, n_chains, s, &a.g.work))) return rc;
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
     return with_path(path, K, [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
@@ -1838,7 +1867,7 @@ int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, dou
   int W;
   if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
   WorkTables wt;
-  if ((rc = wt.get(K_max, n, s, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K_max, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -1878,7 +1907,7 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
     const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
     return dispatch_k<EnergyLaunch>(K_max, grid, block, lds, s, a);
   }
-  if (path || K_max > kMaxKLds) {
+  if (path || K_max >= kWinGlobalFromK) {
     if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
   } else {  // potential-only windowed tables, as launch_energy
     W = 4;
@@ -1900,7 +1929,7 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   a.rows = d_rows;
   a.ld = ld;
   WorkTables wt;
-  if ((rc = wt.get(K_max, n, s, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   auto go = [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2272,7 +2301,7 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   WorkTables wt;
-  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
   return with_path(path, K, [&](auto gt, auto st) {
@@ -2377,7 +2406,7 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
   WorkTables wt;
-  if ((rc = wt.get(K, n, s, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2747,7 +2776,7 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.with_metric = kind;
   a.g = make_geometry(ctx->rows, ctx->cols);
   WorkTables wt;
-  if ((rc = wt.get(K, n_chains, ctx->stream, &a.g.work))) return rc;
+  if ((rc = wt.get(path, K, n_chains, ctx->stream, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
     rc = with_path(path, K, [&](auto gt, auto st) {

@@ -13,10 +13,10 @@
 // Stars.  One wave per chain; star k lives in lane k % 64, register slot
 // k / 64 (SLOTS = 1, 2, 4: K <= 64, 128, 256 — the reference takes any
 // 3 * Nobjs, and its own drivers run K = 100 and grow K to N_max = 120 by
-// births: RHMC-big-sim3.py:18-19, RHMC-big-sim4.py:77).  Beyond 256 stars
-// (SLOTS = 8, 16: K <= 512, 1024) the tables no longer fit LDS and live in
-// global memory (WinGG below); those register states spill to scratch — a
-// completeness path, not a tuned one.
+// births: RHMC-big-sim3.py:18-19, RHMC-big-sim4.py:77).  From 65 stars the
+// launcher takes WinGG below (the tables in global memory: LDS-sized tables
+// cap a CU at one or two waves); beyond 256 stars (SLOTS = 8, 16: K <= 512,
+// 1024) the register states spill to scratch — a completeness path.
 //
 // Gradient, star-major: for star k (wave-uniform), lane (r = l>>5, c = l&31)
 // owns window column c and rows r, r+2, .., r+30 (16 pixels); Lambda at those
@@ -493,12 +493,12 @@ struct WinEG {
   }
 };
 
-// K > 256 (SLOTS 8 / 16): WinG's gradient and potential with each chain's
-// factor tables in global memory — work + (launch wave) x 2 K 33 doubles,
-// 0.5 MB per chain at K = 1024, allocated by the launcher on the launch's
-// stream (Geometry::work) — and only the exp table in LDS.  The tables stay
-// in L2 / HBM, the state spills: correctness at any star count the windowed
-// bound allows, not a tuned kernel (the reference's drivers stop at 120).
+// From 65 stars on the windowed path (SLOTS 2 / 4 / 8 / 16): WinG's gradient
+// and potential with each chain's factor tables in global memory — work +
+// (launch wave) x 2 K 33 doubles, 0.5 MB per chain at K = 1024, allocated by
+// the launcher on the launch's stream (Geometry::work) — and only the exp
+// table in LDS, so four waves share a workgroup (1.3-1.8x the LDS-table
+// kernel from 100 to 200 stars).  Past 256 stars the state spills.
 struct WinGG {
   static __host__ __device__ size_t lds_bytes(int, int) { return kExpTab * sizeof(double); }
   static __host__ __device__ size_t work_doubles(int K) { return win_table_doubles(K); }

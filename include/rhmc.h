@@ -211,11 +211,12 @@ int rhmc_ctx_synchronize(rhmc_ctx* ctx);
  * updated in place.  fp_iters (nullable): host int32 [n_chains][2], the
  * p- and q-loop iteration counts summed over the n_steps steps.  status
  * (nullable): host int32 [n_chains], RHMC_STATUS_* bits.  1 <= K <= 1024 on
- * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).  Past
- * 256 stars the one-wave-per-chain kernels keep their windowed PSF factor
- * tables in global memory, 2 x 33 doubles per star per chain allocated on the
- * call's stream for the launch (RHMC_ERR_NOMEM if that fails), and need a
- * PSF narrow enough for the 32-pixel window (else RHMC_ERR_UNSUPPORTED).
+ * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).  From
+ * 65 stars the windowed one-wave-per-chain kernels (images other than the
+ * dense kernel's 32/48 px, or K > 256) keep their PSF factor tables in global
+ * memory, 2 x 33 doubles per star per chain allocated on the call's stream
+ * for the launch (RHMC_ERR_NOMEM if that fails); they need a PSF narrow
+ * enough for the 32-pixel window (else RHMC_ERR_UNSUPPORTED).
  */
 int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p,
                   int64_t n_chains, int32_t K, int32_t n_steps,

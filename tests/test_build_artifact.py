@@ -56,7 +56,7 @@ SCRATCH_BUDGET = [
     # completeness path past LDS-sized tables; 8 or 16 stars' state per lane
     # does not fit the register file and spills (no BASELINE config or
     # reference driver runs it: the reference's drivers stop at 120 stars)
-    (r"_win_kernel<rhmc::WinGG, (\d, )?(8|16)>", 1300),
+    (r"_win_kernel<rhmc::WinGG, (\d, )?(2|4|8|16)>", 1300),
 ]
 
 
