@@ -25,7 +25,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "rhmc.h"
 #include "rhmc_datagen.hpp"
@@ -46,7 +48,7 @@ namespace rhmc {
 struct Geometry {
   int rows, cols, npix, npl;  // npl = ceil(npix / 64) pixels per lane
   int di, dj;                 // pixel index step of 64 as (rows, cols)
-  double* work;               // WinGG's per-chain factor tables (K > 256), else null
+  double* work;               // WinGG's per-chain factor tables (from 65 stars), else null
 };
 
 struct Tables {  // per-wave LDS tables, K stars
@@ -1040,6 +1042,14 @@ struct rhmc_ctx {
   int kernel = RHMC_KERNEL_AUTO;   // RHMC_OPT_KERNEL
   int mh_fused = 1;                // RHMC_OPT_MH_FUSED
   int window_split = 0;            // RHMC_OPT_WINDOW_SPLIT (0: by batch size)
+  // WinGG factor tables, one buffer per stream (work_tables)
+  struct StreamTables {
+    hipStream_t s;
+    void* p;
+    size_t bytes;
+  };
+  mutable std::mutex tab_mu;
+  mutable std::vector<StreamTables> tabs;
 };
 
 namespace {
@@ -1082,30 +1092,43 @@ int win_slots(int K) {
   return K <= 64 ? 1 : K <= 128 ? 2 : K <= 256 ? 4 : K <= 512 ? 8 : 16;
 }
 
-// WinGG's per-chain factor tables (K > 256) for the n chains of one launch:
-// allocated on the launch's stream and released behind it (stream-ordered,
-// so the launch that reads them has finished first).
-struct WorkTables {
-  void* p = nullptr;
-  hipStream_t s = nullptr;
-  // path: the launch's gradient path (0 = windowed); tables only for WinGG
-  int get(int path, int K, int64_t n, hipStream_t st, double** out) {
-    *out = nullptr;
-    if (path != 0 || K < kWinGlobalFromK || n <= 0) return RHMC_OK;
-    s = st;
-    const size_t bytes = (size_t)n * WinGG::work_doubles(K) * sizeof(double);
-    if (hipMallocAsync(&p, bytes, st) != hipSuccess) {
-      p = nullptr;
-      return fail(RHMC_ERR_NOMEM, "hipMallocAsync of " + std::to_string(bytes) +
-                                      " B of windowed factor tables failed");
-    }
-    *out = (double*)p;
+// WinGG's per-chain factor tables (from kWinGlobalFromK stars): one buffer per
+// (context, stream), grown on demand and kept until rhmc_ctx_destroy. Launches on
+// one stream run in order, so reusing the buffer across them is safe; growing it
+// waits for the stream before the old buffer is released. (Round 5 first took a
+// stream-ordered pool allocation per launch, hipMallocAsync/hipFreeAsync, and the
+// MH bench gave run-to-run different acceptance with it -- DESIGN.md section 4a.)
+int work_tables(const rhmc_ctx* ctx, int path, int K, int64_t n, hipStream_t st,
+                double** out) {
+  *out = nullptr;
+  if (path != 0 || K < kWinGlobalFromK || n <= 0) return RHMC_OK;
+  const size_t bytes = (size_t)n * WinGG::work_doubles(K) * sizeof(double);
+  std::lock_guard<std::mutex> lk(ctx->tab_mu);
+  rhmc_ctx::StreamTables* t = nullptr;
+  for (auto& e : ctx->tabs)
+    if (e.s == st) t = &e;
+  if (t && t->bytes >= bytes) {
+    *out = (double*)t->p;
     return RHMC_OK;
   }
-  ~WorkTables() {
-    if (p) (void)hipFreeAsync(p, s);
+  if (t) {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipFree(t->p));
+    t->p = nullptr;
+    t->bytes = 0;
+  } else {
+    ctx->tabs.push_back({st, nullptr, 0});
+    t = &ctx->tabs.back();
   }
-};
+  if (hipMalloc(&t->p, bytes) != hipSuccess) {
+    t->p = nullptr;
+    return fail(RHMC_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) +
+                                    " B of windowed factor tables failed");
+  }
+  t->bytes = bytes;
+  *out = (double*)t->p;
+  return RHMC_OK;
+}
 
 template <class G, int SLOTS>
 void launch_integrate_win(int32_t solver, dim3 grid, dim3 block, size_t lds, hipStream_t s,
@@ -1542,8 +1565,7 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.K = K;
   a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
   a.g = make_geometry(ctx->rows, ctx->cols);
-  WorkTables wt;
-  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
     auto go = [&](auto gt, auto st) {
@@ -1750,8 +1772,7 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.K = K;
     a.n_steps = n_steps;
     if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
-    WorkTables wt;
-    if ((rc = wt.get(path, K, n_chains, s, &a.g.work))) return rc;
+    if ((rc = work_tables(ctx, path, K, n_chains, s, &a.g.work))) return rc;
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
     return with_path(path, K, [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
@@ -1866,8 +1887,7 @@ int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, dou
   size_t lds;
   int W;
   if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
-  WorkTables wt;
-  if ((rc = wt.get(path, K_max, n, s, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K_max, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -1928,8 +1948,7 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   a.Kc = d_K;
   a.rows = d_rows;
   a.ld = ld;
-  WorkTables wt;
-  if ((rc = wt.get(path, K_max, n, s, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   auto go = [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2300,8 +2319,7 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
-  WorkTables wt;
-  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
   return with_path(path, K, [&](auto gt, auto st) {
@@ -2405,8 +2423,7 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
-  WorkTables wt;
-  if ((rc = wt.get(path, K, n, s, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2606,6 +2623,9 @@ void rhmc_ctx_destroy(rhmc_ctx* ctx) {
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->mh_scratch) (void)hipFree(ctx->mh_scratch);
+  if (!ctx->tabs.empty()) (void)hipDeviceSynchronize();   // tables may serve user streams
+  for (auto& t : ctx->tabs)
+    if (t.p) (void)hipFree(t.p);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -2775,8 +2795,7 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.K = K;
   a.with_metric = kind;
   a.g = make_geometry(ctx->rows, ctx->cols);
-  WorkTables wt;
-  if ((rc = wt.get(path, K, n_chains, ctx->stream, &a.g.work))) return rc;
+  if ((rc = work_tables(ctx, path, K, n_chains, ctx->stream, &a.g.work))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
     rc = with_path(path, K, [&](auto gt, auto st) {

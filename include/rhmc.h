@@ -63,9 +63,9 @@
  *   - Every call returns 0 on success or a negative RHMC_ERR_* code;
  *     rhmc_last_error() gives a thread-local message.  No C++ exception
  *     crosses the ABI.  A context must not be used by two threads at once,
- *     except that rhmc_leapfrog_device and rhmc_energy_device (which keep no
- *     per-call state in the context) may be called from several threads on
- *     distinct streams; one context per GPU.
+ *     except that rhmc_leapfrog_device and rhmc_energy_device (whose only
+ *     state in the context is a per-stream, mutex-guarded table buffer) may be
+ *     called from several threads on distinct streams; one context per GPU.
  */
 #ifndef RHMC_H
 #define RHMC_H
@@ -214,8 +214,9 @@ int rhmc_ctx_synchronize(rhmc_ctx* ctx);
  * every step, gradient, energy and MH entry point (else RHMC_ERR_ARG).  From
  * 65 stars the windowed one-wave-per-chain kernels (images other than the
  * dense kernel's 32/48 px, or K > 256) keep their PSF factor tables in global
- * memory, 2 x 33 doubles per star per chain allocated on the call's stream
- * for the launch (RHMC_ERR_NOMEM if that fails); they need a PSF narrow
+ * memory, 2 x 33 doubles per star per chain in a buffer the context keeps
+ * per stream until rhmc_ctx_destroy (grown on demand after a sync of that
+ * stream; RHMC_ERR_NOMEM if that fails); they need a PSF narrow
  * enough for the 32-pixel window (else RHMC_ERR_UNSUPPORTED).
  */
 int rhmc_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* q, double* p,

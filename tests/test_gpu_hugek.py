@@ -1,7 +1,7 @@
 """K > 256 stars per chain through the C-ABI: the slotted one-wave-per-chain
 kernels at 8 and 16 register slots (up to 512 / 1024 stars) with their
 windowed factor tables in global memory (rhmc_windowed.hpp WinGG; allocated
-per launch on the launch's stream).  The reference's dVdq / V /
+in a per-stream buffer of the context).  The reference's dVdq / V /
 RHMC_single_step take any 3 * Nobjs (sampler_RHMC.py:365-425, :294-351,
 :522-566); its own drivers stop at 120 stars, so this is the completeness
 path, not a tuned one.
