@@ -81,3 +81,45 @@ def test_windowed_global_tables_two_streams_in_flight(gpu_lib):
         assert np.array_equal(q, qs)
         assert np.array_equal(p, ps)
     ctx.close()
+
+
+def test_windowed_global_tables_two_threads(gpu_lib):
+    """rhmc_leapfrog_device from two host threads on distinct streams of one
+    context (include/rhmc.h: allowed; the table buffers are per stream behind a
+    mutex): each thread's chains equal a serial launch."""
+    import threading
+    capi = gpu_lib
+    wl = workloads.make("S256K100", n_chains=1024)
+    P = capi.make_params(**wl.params)
+    dev = torch.device("cuda", 0)
+    ctx = capi.Context(wl.D)
+    q0 = torch.from_numpy(wl.q0).to(dev)
+    p0 = torch.from_numpy(wl.p0).to(dev)
+    serial = (q0.clone(), p0.clone())
+    for _ in range(3):
+        ctx.leapfrog_device(P, serial[0].data_ptr(), serial[1].data_ptr(), wl.n_chains, wl.K, 2)
+    torch.cuda.synchronize()
+    outs = [(q0.clone(), p0.clone()) for _ in range(2)]
+    streams = [torch.cuda.Stream(dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    errs = []
+
+    def work(i):
+        try:
+            for _ in range(3):   # 2 + 2 + 2 steps
+                ctx.leapfrog_device(P, outs[i][0].data_ptr(), outs[i][1].data_ptr(),
+                                    wl.n_chains, wl.K, 2, stream=streams[i].cuda_stream)
+        except Exception as e:  # noqa: BLE001 - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs
+    for q, p in outs:
+        assert np.array_equal(q.cpu().numpy(), serial[0].cpu().numpy())
+        assert np.array_equal(p.cpu().numpy(), serial[1].cpu().numpy())
+    ctx.close()
