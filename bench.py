@@ -431,7 +431,7 @@ def main():
                          "rj: the reversible-jump run_RHMC through librhmc_rj.so, one step "
                          "= --mh-iter iterations of --leap steps (default workload: use B4)")
     ap.add_argument("--mh-iter", type=int, default=10)
-    ap.add_argument("--rj-pipes", type=int, choices=(0, 1, 2, 3, 4), default=0,
+    ap.add_argument("--rj-pipes", type=int, choices=tuple(range(9)), default=0,
                     help="--mode rj: host pipes of the native driver (0: its default)")
     ap.add_argument("--f-pos", type=int, choices=(0, 1), default=1,
                     help="--mode mh: run_RHMC's f_pos (V = inf below the flux wall, "

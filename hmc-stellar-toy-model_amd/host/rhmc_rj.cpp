@@ -40,7 +40,7 @@
 
 namespace {
 
-constexpr int kMaxPipes = 4;  // rhmc_rj_config::n_pipes
+constexpr int kMaxPipes = 8;  // rhmc_rj_config::n_pipes
 
 thread_local std::string g_err;
 
@@ -452,7 +452,7 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
   if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
   if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
   if (cfg->n_pipes < 0 || cfg->n_pipes > kMaxPipes)
-    return fail(RHMC_ERR_ARG, "n_pipes must be in [0, 4]");
+    return fail(RHMC_ERR_ARG, "n_pipes must be in [0, 8]");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
   if (n > 0 && (!q || !K)) return fail(RHMC_ERR_ARG, "q or K is NULL");
   if (cfg->use_states != 0 && cfg->use_states != 1)
@@ -1306,9 +1306,12 @@ int pipes_for(const rhmc_rj_config* cfg, int64_t n) {
   // 1.80e7 / 2.06e7 / 2.12e7.  After the ragged pixel-major launches
   // (profiles/r05_pipes2/, r05_pipes3/, four repeats): 4,096 chains B4 2.62e7 /
   // 2.72e7 with 3 / 4 pipes, the flagship 2.64e7 / 2.78e7; 6 and 8 pipes
-  // (more streams than the box's 4 hardware queues) 0.75-0.95x
-  int pipes = cfg->n_pipes > 0 ? cfg->n_pipes
-                               : (n >= 4096 ? 4 : n >= 2048 ? 3 : n >= 1024 ? 2 : 1);
+  // (more streams than the box's 4 hardware queues) 0.75-0.95x.  At 16,384
+  // chains 8 pipes beat 4 (profiles/r05_pipes8/, two repeats): B4 3.28e7 /
+  // 3.18e7 against 2.94e7 / 2.82e7 (4,096 chains: 0.6x)
+  int pipes = cfg->n_pipes > 0
+                  ? cfg->n_pipes
+                  : (n >= 16384 ? 8 : n >= 4096 ? 4 : n >= 2048 ? 3 : n >= 1024 ? 2 : 1);
   return (int)std::max<int64_t>(1, std::min<int64_t>(pipes, n));
 }
 

@@ -708,8 +708,8 @@ class multi_gym(base_class):
         (include/rhmc_rj.h): per-chain host work in C++ on n_threads host
         threads (0: up to 16) with a bit-identical replica of each chain's
         NumPy stream, and flag_chain [Niter+1, n] marks the iterations whose
-        proposal was a dead end (see the header); n_pipes = 2..4 (the default:
-        2 from 1,024 chains, 3 from 2,048, 4 from 4,096) runs the chains in
+        proposal was a dead end (see the header); n_pipes = 2..8 (the default:
+        2 from 1,024 chains, 3 from 2,048, 4 from 4,096, 8 from 16,384) runs the chains in
         that many parts whose host and GPU phases overlap, 1 in one pass;
         rng_states (native only): the chains' streams to start from instead of
         the seeds — a list of numpy RandomState objects or the rj_rng_states

@@ -96,10 +96,11 @@ typedef struct rhmc_rj_config {
   int32_t n_threads;     /* host worker threads; <= 0: min(hardware threads, 16)    */
   int32_t n_g_ff2;       /* schedule_g_ff2 length (0: none)                          */
   int32_t n_beta;        /* schedule_beta length (0: none)                           */
-  int32_t n_pipes;       /* 1: one pass over all chains per phase; 2..4: the chains in
+  int32_t n_pipes;       /* 1: one pass over all chains per phase; 2..8: the chains in
                             that many contiguous parts on as many host threads, so
                             one part's host work overlaps the others' GPU work; 0:
-                            2 from 1,024 chains, 3 from 2,048, 4 from 4,096          */
+                            2 from 1,024 chains, 3 from 2,048, 4 from 4,096, 8 from
+                            16,384                                                    */
   int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
                             seeds[c] (a checkpoint of an earlier run, or any
                             RandomState's get_state(): continue its stream)        */

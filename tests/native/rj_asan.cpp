@@ -252,7 +252,7 @@ int main(int argc, char** argv) {
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "reserved");
     c = config(2, 4, 0.5, 0.25, 0.25);
-    c.n_pipes = 5;
+    c.n_pipes = 9;
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "n_pipes");
     c = config(2, 4, 0.5, 0.25, 0.25);
