@@ -357,6 +357,9 @@ def bench_rj(args, wl, gpu, world, rank):
     # packs it in one native pass)
     starts = np.stack(starts)
     seeds = [1000 * rank + c for c in range(n_chains)]
+    # successive runs write their q_chain / p_chain records into the previous
+    # run's arrays (opt-in: no page faults on fresh memory inside the timing)
+    kw["reuse_records"] = True
     for _ in range(args.warmup):
         g.run_RHMC_rj_batched(starts, seeds, n_pipes=args.rj_pipes, **kw)
     if world > 1:
@@ -444,6 +447,11 @@ def main():
     ap.add_argument("--window-split", type=int, choices=(0, 1, 2, 4), default=0,
                     help="RHMC_OPT_WINDOW_SPLIT for the multi-star register-window kernel "
                          "(0: by batch size; results bit-identical)")
+    ap.add_argument("--tables", type=int, choices=(0, 1, 2, 3, 4, 5), default=0,
+                    help="RHMC_OPT_TABLES (diagnostic): 0 per-stream buffer, 1 the same "
+                         "NaN-filled before each launch, 2 / 3 per-launch pool allocation "
+                         "without / with the fill, 4 pool allocation never reused, 5 pool "
+                         "allocation freed after a stream sync")
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
     ap.add_argument("--n-real", type=int, default=1000)
     ap.add_argument("--dry-run", action="store_true",
@@ -524,6 +532,8 @@ def main():
     ctx = capi.Context(wl.D, device=gpu)
     if args.window_split:
         ctx.set_option(capi.OPT_WINDOW_SPLIT, args.window_split)
+    if args.tables:
+        ctx.set_option(capi.OPT_TABLES, args.tables)
     q = torch.from_numpy(wl.q0).to(dev).contiguous()
     p = torch.from_numpy(wl.p0).to(dev).contiguous()
     it = torch.zeros((wl.n_chains, 2), dtype=torch.int32, device=dev)

@@ -39,6 +39,17 @@ namespace rhmc {
 
 // gauss_run8: rhmc_windowed.hpp.
 
+// Two adjacent doubles of LDS in one 16-byte read (ds_read_b128: 4 LDS cycles
+// per wave-instruction at 256 B/clk/CU, where the two 8-byte reads the
+// compiler forms without the alignment, ds_read2_b64, take 8 at 128 B/clk).
+// Every such pair below starts on a 16-byte boundary (even double offsets).
+__device__ __forceinline__ void lds_pair(const double* p, double& a, double& b) {
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  const v2d t = *reinterpret_cast<const v2d*>(p);
+  a = t.x;
+  b = t.y;
+}
+
 // Row groups per star in the dense kernel's pass 3 (log2): the G in {1, 2, 4}
 // with the fewest row-units ceil(G K / 64) / G per lane, the smallest on a
 // tie — K <= 16: 4 (a quarter of the rows per lane), K <= 32: 2, K = 100: 4
@@ -69,11 +80,15 @@ struct DenseG {
   // the rows of pass-3 row group g shifted by 2 g doubles (16 g bytes), so
   // the G groups' simultaneous row reads hit different banks.
   static constexpr int TP = IMG + 2;
+  // lds_pair's 16-byte alignment: every region and row offset an even double count
+  static_assert(BS % 2 == 0 && TP % 2 == 0 && IMG % 2 == 0 && kExpTab % 2 == 0 && CW % 2 == 0,
+                "16-byte LDS pairs");
   // per wave: the tile tables ex [TK][TP] + fey [TK][TP], later s (+ skews)
   static __host__ __device__ constexpr size_t wave_doubles() {
     return 2 * TK * TP > IMG * IMG + 8 ? (size_t)2 * TK * TP : (size_t)IMG * IMG + 8;
   }
   // LDS: exp table, the image (fp64, [IMG][IMG]), the waves' regions
+  static_assert(wave_doubles() % 2 == 0, "16-byte LDS pairs");
   static __host__ __device__ constexpr size_t lds_bytes(int waves) {
     return (kExpTab + (size_t)IMG * IMG + (size_t)waves * wave_doubles()) * sizeof(double);
   }
@@ -147,9 +162,9 @@ struct DenseG {
       for (int r = 0; r < nk; ++r) {  // stars in ascending order
         double ex[BS], fy[BS];
 #pragma unroll
-        for (int u = 0; u < BS; ++u) ex[u] = ext[r * TP + a * BS + u];
+        for (int u = 0; u < BS; u += 2) lds_pair(ext + r * TP + a * BS + u, ex[u], ex[u + 1]);
 #pragma unroll
-        for (int v = 0; v < BS; ++v) fy[v] = fyt[r * TP + b * BS + v];
+        for (int v = 0; v < BS; v += 2) lds_pair(fyt + r * TP + b * BS + v, fy[v], fy[v + 1]);
 #pragma unroll
         for (int u = 0; u < BS; ++u)
 #pragma unroll
@@ -185,8 +200,10 @@ struct DenseG {
         for (int v = 0; v < BS; v += 2) {
           const double l0 = lam[u * BS + v], l1 = lam[u * BS + v + 1];
           const double r = rcp_nr1(l0 * l1);
-          srow[v] = fma(drow[v], l1 * r, -1.0);
-          srow[v + 1] = fma(drow[v + 1], l0 * r, -1.0);
+          double d0, d1;
+          lds_pair(drow + v, d0, d1);
+          srow[v] = fma(d0, l1 * r, -1.0);
+          srow[v + 1] = fma(d1, l0 * r, -1.0);
         }
       }
     }
@@ -236,7 +253,8 @@ struct DenseG {
             double r0 = 0.0, r1 = 0.0;
 #pragma unroll
             for (int j = 0; j < CW; j += 2) {
-              const double s0 = sr[j], s1 = sr[j + 1];
+              double s0, s1;
+              lds_pair(sr + j, s0, s1);
               r0 = fma(ey[j], s0, r0);
               r1 = fma(ey[j + 1], s1, r1);
               C[j] = fma(ex[l], s0, C[j]);

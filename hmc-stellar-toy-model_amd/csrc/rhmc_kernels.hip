@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1042,14 +1043,35 @@ struct rhmc_ctx {
   int kernel = RHMC_KERNEL_AUTO;   // RHMC_OPT_KERNEL
   int mh_fused = 1;                // RHMC_OPT_MH_FUSED
   int window_split = 0;            // RHMC_OPT_WINDOW_SPLIT (0: by batch size)
-  // WinGG factor tables, one buffer per stream (work_tables)
+  int table_mode = RHMC_TABLES_STREAM;  // RHMC_OPT_TABLES (diagnostic modes, rhmc.h)
+  // WinGG factor tables, one buffer per stream (work_tables).  A launch holds a
+  // lease (shared_ptr) on its buffer from the lookup until the launch is
+  // enqueued, so a concurrent grow on the same stream cannot free it early.
+  struct TabBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipStream_t s = nullptr;
+    bool pooled = false;   // RHMC_TABLES_POOL*: stream-ordered, freed behind the launch
+    bool synced = false;   // rhmc_ctx_destroy synchronised the device already
+    bool sync_free = false;  // pooled: wait for the stream before hipFreeAsync
+    ~TabBuf() {
+      if (!p) return;
+      if (pooled) {
+        if (sync_free) (void)hipStreamSynchronize(s);  // RHMC_TABLES_POOL_SYNCFREE
+        (void)hipFreeAsync(p, s);
+        return;
+      }
+      if (!synced) (void)hipStreamSynchronize(s);  // the last launch reading it
+      (void)hipFree(p);
+    }
+  };
   struct StreamTables {
     hipStream_t s;
-    void* p;
-    size_t bytes;
+    std::shared_ptr<TabBuf> buf;
   };
   mutable std::mutex tab_mu;
   mutable std::vector<StreamTables> tabs;
+  mutable std::vector<std::shared_ptr<TabBuf>> kept;  // RHMC_TABLES_POOL_KEEP
 };
 
 namespace {
@@ -1093,40 +1115,73 @@ int win_slots(int K) {
 }
 
 // WinGG's per-chain factor tables (from kWinGlobalFromK stars): one buffer per
-// (context, stream), grown on demand and kept until rhmc_ctx_destroy. Launches on
-// one stream run in order, so reusing the buffer across them is safe; growing it
-// waits for the stream before the old buffer is released. (Round 5 first took a
-// stream-ordered pool allocation per launch, hipMallocAsync/hipFreeAsync, and the
-// MH bench gave run-to-run different acceptance with it -- DESIGN.md section 4a.)
+// (context, stream), grown on demand and kept until rhmc_ctx_destroy.  Launches
+// on one stream run in order, so they can share it.  The caller keeps `lease`
+// alive until its launch is enqueued: a grow by another thread on the same
+// stream then replaces the context's buffer, and the old one is released only
+// when its last lease goes (after a sync of its stream).  Every region a launch
+// uses is written by that launch before it is read (win_build_tables,
+// win_build_ey), which RHMC_TABLES_POISON checks.
+using TableLease = std::shared_ptr<rhmc_ctx::TabBuf>;
+
 int work_tables(const rhmc_ctx* ctx, int path, int K, int64_t n, hipStream_t st,
-                double** out) {
+                double** out, TableLease* lease) {
   *out = nullptr;
+  lease->reset();
   if (path != 0 || K < kWinGlobalFromK || n <= 0) return RHMC_OK;
   const size_t bytes = (size_t)n * WinGG::work_doubles(K) * sizeof(double);
+  const int mode = ctx->table_mode;
+  const bool poison = mode == RHMC_TABLES_STREAM_POISON || mode == RHMC_TABLES_POOL_POISON;
+  if (mode == RHMC_TABLES_POOL || mode == RHMC_TABLES_POOL_POISON ||
+      mode == RHMC_TABLES_POOL_KEEP || mode == RHMC_TABLES_POOL_SYNCFREE) {
+    // Diagnostic: round 5's first scheme, one stream-ordered pool allocation
+    // per launch, released behind it (~TabBuf: hipFreeAsync on st).
+    auto b = std::make_shared<rhmc_ctx::TabBuf>();
+    b->s = st;
+    b->pooled = true;
+    b->sync_free = mode == RHMC_TABLES_POOL_SYNCFREE;
+    if (hipMallocAsync(&b->p, bytes, st) != hipSuccess) {
+      b->p = nullptr;
+      return fail(RHMC_ERR_NOMEM, "hipMallocAsync of " + std::to_string(bytes) +
+                                      " B of windowed factor tables failed");
+    }
+    b->bytes = bytes;
+    if (poison) HIP_TRY(hipMemsetAsync(b->p, 0xFF, bytes, st));
+    *out = (double*)b->p;
+    if (mode == RHMC_TABLES_POOL_KEEP) {  // never reused: released at rhmc_ctx_destroy
+      std::lock_guard<std::mutex> lk(ctx->tab_mu);
+      ctx->kept.push_back(b);
+    }
+    *lease = std::move(b);
+    return RHMC_OK;
+  }
   std::lock_guard<std::mutex> lk(ctx->tab_mu);
   rhmc_ctx::StreamTables* t = nullptr;
   for (auto& e : ctx->tabs)
     if (e.s == st) t = &e;
-  if (t && t->bytes >= bytes) {
-    *out = (double*)t->p;
-    return RHMC_OK;
+  if (!t || !t->buf || t->buf->bytes < bytes) {
+    auto b = std::make_shared<rhmc_ctx::TabBuf>();
+    b->s = st;
+    if (hipMalloc(&b->p, bytes) != hipSuccess) {
+      b->p = nullptr;
+      return fail(RHMC_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) +
+                                      " B of windowed factor tables failed");
+    }
+    b->bytes = bytes;
+    if (t)
+      t->buf = std::move(b);  // the old buffer goes with its last lease
+    else
+      ctx->tabs.push_back({st, std::move(b)});
+    t = nullptr;
+    for (auto& e : ctx->tabs)
+      if (e.s == st) t = &e;
   }
-  if (t) {
-    HIP_TRY(hipStreamSynchronize(st));
-    HIP_TRY(hipFree(t->p));
-    t->p = nullptr;
-    t->bytes = 0;
-  } else {
-    ctx->tabs.push_back({st, nullptr, 0});
-    t = &ctx->tabs.back();
-  }
-  if (hipMalloc(&t->p, bytes) != hipSuccess) {
-    t->p = nullptr;
-    return fail(RHMC_ERR_NOMEM, "hipMalloc of " + std::to_string(bytes) +
-                                    " B of windowed factor tables failed");
-  }
-  t->bytes = bytes;
-  *out = (double*)t->p;
+  // 0xFF bytes are NaN doubles: a read of an entry this launch did not write
+  // turns its chain's result NaN (status NONFINITE) instead of reusing a
+  // previous launch's value.
+  if (poison) HIP_TRY(hipMemsetAsync(t->buf->p, 0xFF, bytes, st));
+  *out = (double*)t->buf->p;
+  *lease = t->buf;
   return RHMC_OK;
 }
 
@@ -1565,7 +1620,8 @@ int launch_energy(const rhmc_ctx* ctx, const Consts& c, const double* d_q, const
   a.K = K;
   a.f_pos = f_pos & (RHMC_V_FLUX_WALL | RHMC_V_NO_POSCHECK);
   a.g = make_geometry(ctx->rows, ctx->cols);
-  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   if (win) {
     auto go = [&](auto gt, auto st) {
@@ -1772,7 +1828,8 @@ int launch_leapfrog(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, double* d_
     a.K = K;
     a.n_steps = n_steps;
     if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
-    if ((rc = work_tables(ctx, path, K, n_chains, s, &a.g.work))) return rc;
+    TableLease lease;
+    if ((rc = work_tables(ctx, path, K, n_chains, s, &a.g.work, &lease))) return rc;
     const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
     return with_path(path, K, [&](auto gt, auto st) {
       using G = typename decltype(gt)::type;
@@ -1887,7 +1944,8 @@ int launch_leapfrog_ragged(rhmc_ctx* ctx, const rhmc_params* P, double* d_q, dou
   size_t lds;
   int W;
   if ((rc = pick_waves_path(ctx, path, K_max, &lds, &W))) return rc;
-  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K_max, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -1948,7 +2006,8 @@ int launch_energy_ragged(rhmc_ctx* ctx, const rhmc_params* P, const double* d_q,
   a.Kc = d_K;
   a.rows = d_rows;
   a.ld = ld;
-  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K_max, n, s, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   auto go = [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2319,7 +2378,8 @@ int launch_integrate(rhmc_ctx* ctx, const rhmc_params* P, int32_t solver, double
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
-  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   const int fp = f_pos != 0;
   return with_path(path, K, [&](auto gt, auto st) {
@@ -2423,7 +2483,8 @@ int launch_hmc_random(rhmc_ctx* ctx, const rhmc_params* P, const double* d_dt, d
   int W;
   if (int rc = pick_waves_path(ctx, path, K, &lds, &W)) return rc;
   HIP_TRY(hipSetDevice(ctx->device));
-  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K, n, s, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n + W - 1) / W)), block(W * kWave);
   return with_path(path, K, [&](auto gt, auto st) {
     using G = typename decltype(gt)::type;
@@ -2593,6 +2654,11 @@ int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value) {
         return fail(RHMC_ERR_ARG, "RHMC_OPT_WINDOW_SPLIT must be 0, 1, 2 or 4");
       ctx->window_split = value;
       return RHMC_OK;
+    case RHMC_OPT_TABLES:
+      if (value < RHMC_TABLES_STREAM || value > RHMC_TABLES_POOL_SYNCFREE)
+        return fail(RHMC_ERR_ARG, "RHMC_OPT_TABLES must be 0 ... 5");
+      ctx->table_mode = value;
+      return RHMC_OK;
     default:
       return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
   }
@@ -2604,6 +2670,7 @@ int rhmc_ctx_get_option(rhmc_ctx* ctx, int32_t option, int32_t* value) {
     case RHMC_OPT_KERNEL: *value = ctx->kernel; return RHMC_OK;
     case RHMC_OPT_MH_FUSED: *value = ctx->mh_fused; return RHMC_OK;
     case RHMC_OPT_WINDOW_SPLIT: *value = ctx->window_split; return RHMC_OK;
+    case RHMC_OPT_TABLES: *value = ctx->table_mode; return RHMC_OK;
     default: return fail(RHMC_ERR_ARG, "unknown option " + std::to_string(option));
   }
 }
@@ -2623,9 +2690,13 @@ void rhmc_ctx_destroy(rhmc_ctx* ctx) {
   if (ctx->d_flag) (void)hipFree(ctx->d_flag);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->mh_scratch) (void)hipFree(ctx->mh_scratch);
-  if (!ctx->tabs.empty()) (void)hipDeviceSynchronize();   // tables may serve user streams
+  if (!ctx->tabs.empty() || !ctx->kept.empty())
+    (void)hipDeviceSynchronize();   // tables may serve user streams
   for (auto& t : ctx->tabs)
-    if (t.p) (void)hipFree(t.p);
+    if (t.buf) t.buf->synced = true;  // user streams may be gone: no per-stream sync
+  for (auto& b : ctx->kept) b->s = nullptr;  // pool frees after the device sync above
+  ctx->tabs.clear();
+  ctx->kept.clear();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -2795,7 +2866,8 @@ int rhmc_gradient(rhmc_ctx* ctx, const rhmc_params* P, const double* q, double* 
   a.K = K;
   a.with_metric = kind;
   a.g = make_geometry(ctx->rows, ctx->cols);
-  if ((rc = work_tables(ctx, path, K, n_chains, ctx->stream, &a.g.work))) return rc;
+  TableLease lease;
+  if ((rc = work_tables(ctx, path, K, n_chains, ctx->stream, &a.g.work, &lease))) return rc;
   const dim3 grid((unsigned)((n_chains + W - 1) / W)), block(W * kWave);
   if (win) {
     rc = with_path(path, K, [&](auto gt, auto st) {
@@ -3071,4 +3143,17 @@ int rhmc_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* q, int32_t
   return RHMC_OK;
 }
 
+#ifdef RHMC_TABLE_CANARY
+// Diagnostic builds only (not declared in rhmc.h): the table-region conflicts
+// seen since the last call, [total, in gradients, in potentials]; resets them.
+int rhmc_debug_table_conflicts(int64_t* out3) {
+  unsigned long long h[3] = {0, 0, 0};
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tab_conflicts), sizeof(h)));
+  const unsigned long long z[3] = {0, 0, 0};
+  HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_tab_conflicts), z, sizeof(z)));
+  for (int i = 0; i < 3; ++i) out3[i] = (int64_t)h[i];
+  return RHMC_OK;
+}
+#endif
 }  // extern "C"

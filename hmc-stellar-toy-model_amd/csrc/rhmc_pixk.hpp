@@ -370,6 +370,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2)))
 leapfrog_pk(LeapArgsKR a, int f_pos) {
   // (HMC_random ran two columns per pass until the unguarded accumulation
   // freed the registers three need)
+  // The all-reduce gradient (RHMC_PK_RS = 0) assumes one K per wave.
+  static_assert(!RAGGED || RHMC_PK_RS, "ragged pixel-major launches need the reduce-scatter");
   using PK = PixK<IMG, KMAX, RHMC_PK_CT>;
   extern __shared__ double lds[];
   const int W = blockDim.x / kWave;

@@ -59,13 +59,46 @@ __device__ __forceinline__ int readlane_i(int v, int src) {
 template <bool GT>
 __device__ __forceinline__ void tab_sync() {
   if constexpr (GT) {
+#ifdef RHMC_GT_FENCE_AGENT  // diagnostic build: agent scope (L1 written back / invalidated)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+#endif
   } else {
     wave_lds_sync();
   }
 }
+
+// Diagnostic build (-DRHMC_TABLE_CANARY, never the product library): each
+// wave's global table region starts with a 64-bit counter that lane 0 bumps
+// when a gradient / potential starts and again when it ends; a bump by
+// anything else in between (another launch using the same region) is counted
+// in g_tab_conflicts, tagged by the kind of call that saw it (1 gradient,
+// 2 potential), and read by rhmc_debug_table_conflicts().
+#ifdef RHMC_TABLE_CANARY
+constexpr int kTabHeader = 8;  // doubles before a wave's tables
+__device__ unsigned long long g_tab_conflicts[3];
+__device__ __forceinline__ unsigned long long canary_enter(double* hdr) {
+  unsigned long long v = 0;
+  if (lane_id() == 0) v = atomicAdd((unsigned long long*)hdr, 1ull);
+  return v;
+}
+__device__ __forceinline__ void canary_leave(double* hdr, unsigned long long v, int kind) {
+  if (lane_id() == 0) {
+    const unsigned long long now = atomicAdd((unsigned long long*)hdr, 1ull);
+    if (now != v + 1ull) {
+      atomicAdd(&g_tab_conflicts[0], 1ull);
+      atomicAdd(&g_tab_conflicts[kind], 1ull);
+    }
+  }
+}
+#else
+constexpr int kTabHeader = 0;
+#endif
 
 // Does lane `lane` hold a star in slot t?
 __device__ __forceinline__ bool win_own(int t, int K) { return kWave * t + lane_id() < K; }
@@ -147,6 +180,9 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
                              const LeanConsts& lc, bool with_metric, double (&gf)[SLOTS],
                              double (&gx)[SLOTS], double (&gy)[SLOTS]) {
   const int lane = lane_id();
+#ifdef RHMC_TABLE_CANARY
+  const unsigned long long cv = GT ? canary_enter(t.ex - kTabHeader) : 0ull;
+#endif
   int bx[SLOTS], by[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
@@ -248,6 +284,9 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
   }
   if (c.use_Vc) vc_gradient<SLOTS>(K, x, y, c, gx, gy);     // :411-418
   tab_sync<GT>();
+#ifdef RHMC_TABLE_CANARY
+  if (GT) canary_leave(t.ex - kTabHeader, cv, 1);
+#endif
 }
 
 // Column factor tables only (the potential's; the row factors are per-row
@@ -328,6 +367,9 @@ __device__ double win_potential(const double* __restrict__ D, double* ey,
                                 const LeanConsts& lc) {
   constexpr int R = kPotRows;
   const int lane = lane_id();
+#ifdef RHMC_TABLE_CANARY
+  const unsigned long long cv = GT ? canary_enter(ey - kTabHeader) : 0ull;
+#endif
   int bx[SLOTS], by[SLOTS];
 #pragma unroll
   for (int s = 0; s < SLOTS; ++s) {
@@ -411,6 +453,9 @@ __device__ double win_potential(const double* __restrict__ D, double* ey,
     }
   }
   tab_sync<GT>();
+#ifdef RHMC_TABLE_CANARY
+  if (GT) canary_leave(ey - kTabHeader, cv, 2);
+#endif
   return wave_sum_dpp(v);
 }
 
@@ -501,14 +546,20 @@ struct WinEG {
 // kernel from 100 to 200 stars).  Past 256 stars the state spills.
 struct WinGG {
   static __host__ __device__ size_t lds_bytes(int, int) { return kExpTab * sizeof(double); }
-  static __host__ __device__ size_t work_doubles(int K) { return win_table_doubles(K); }
+  static __host__ __device__ size_t work_doubles(int K) {
+#ifdef RHMC_TAB_PAD  // diagnostic: each wave's region on whole 128-byte lines
+    return (win_table_doubles(K) + kTabHeader + 15) / 16 * 16;
+#else
+    return win_table_doubles(K) + kTabHeader;
+#endif
+  }
   using Ctx = WinG::Ctx;
   static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,
                                               int cols, double* work) {
     exp_tab_fill(lds);
     __syncthreads();
     const int64_t wave = (int64_t)blockIdx.x * (blockDim.x / kWave) + threadIdx.x / kWave;
-    double* base = work + wave * (int64_t)win_table_doubles(K);
+    double* base = work + wave * (int64_t)work_doubles(K) + kTabHeader;
     Ctx g;
     g.etab = lds;
     g.tab = WinTables{base, base + K * kTabW};

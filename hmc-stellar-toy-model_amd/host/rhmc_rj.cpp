@@ -717,8 +717,8 @@ constexpr int kStreamsPerPipe = 2;  // main (in order) + aux (records, packed gr
 enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions };
 
 // One pipe's buffers: device rows and pinned staging, grown as needed and kept
-// for the process (a run of 4,096 chains at N_max 120 holds ~90 MB of HBM and
-// ~60 MB of pinned memory per pipe).  `mu` is held for a whole run, so two
+// until rhmc_rj_release (a run of 4,096 chains at N_max 120 holds ~90 MB of HBM
+// and ~60 MB of pinned memory per pipe).  `mu` is held for a whole run, so two
 // concurrent rhmc_rj_run calls on one device serialise pipe by pipe.
 struct Work {
   std::mutex mu;
@@ -753,6 +753,22 @@ struct Work {
     Kh = nullptr;
     zoffh = idxh = nullptr;
     cap_n = cap_W = 0;
+  }
+
+  // everything, streams and events included (rhmc_rj_release; `mu` held)
+  void destroy() {
+    if (dev < 0) return;
+    (void)hipSetDevice(dev);
+    for (auto& st : s)
+      if (st) (void)hipStreamSynchronize(st);
+    release();
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& st : s)
+      if (st) (void)hipStreamDestroy(st);
+    for (auto& e : ev) e = nullptr;
+    for (auto& st : s) st = nullptr;
+    dev = -1;
   }
 
   // streams and events on `device` once; buffers for n chains of W doubles
@@ -1056,23 +1072,33 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       h.dead = false;
     });
     lap(0);
-    // 2. device: Q = Q0, p = z sqrt(H(q)), T0; record rows; V(q) unless reused
+    // 2. device: Q = Q0, p = z sqrt(H(q)), T0; record rows; V(q) unless reused.
+    // Rows are zero past 3 K in Q0; Q may hold a rejected birth's or split's
+    // extra star past it (3 entries), so Q = Q0 covers 3 K_max + 3 columns and
+    // every other copy only the columns a row can use (not the 3 N_max width)
+    const int32_t kmax = *std::max_element(Kc.begin(), Kc.end());
+    const int64_t wq = std::min<int64_t>(W, 3 * (int64_t)kmax + 3);
+    const int64_t wr = 3 * (int64_t)kmax;  // the record rows' live columns
     RJ_TRY(D.upload_K());
     RJ_HIP(hipMemcpyAsync(w->Z, w->Zh, (size_t)zt * 8, hipMemcpyHostToDevice, s0));
     RJ_HIP(hipMemcpyAsync(w->zoffd, w->zoffh, (size_t)n * 8, hipMemcpyHostToDevice, s0));
-    RJ_HIP(hipMemcpyAsync(w->Q, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToDevice, s0));
+    RJ_HIP(hipMemcpy2DAsync(w->Q, (size_t)W * 8, w->Q0, (size_t)W * 8, (size_t)wq * 8, (size_t)n,
+                            hipMemcpyDeviceToDevice, s0));
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, w->Z, w->zoffd, n,
                                           w->T0, s0))
       return D.engine_fail(rc, "momentum");
     RJ_HIP(hipMemcpyAsync(w->T0h, w->T0, (size_t)n * 8, hipMemcpyDeviceToHost, s0));
     if (rec_p)
-      RJ_HIP(hipMemcpyAsync(w->Ps, w->P, (size_t)(n * W) * 8, hipMemcpyDeviceToDevice, s0));
-    if (rec_q || rec_p) {  // the record rows leave on the aux stream
+      RJ_HIP(hipMemcpy2DAsync(w->Ps, (size_t)W * 8, w->P, (size_t)W * 8, (size_t)wr * 8,
+                              (size_t)n, hipMemcpyDeviceToDevice, s0));
+    if (rec_q || rec_p) {  // the record rows' live columns leave on the aux stream
       RJ_TRY(D.join(0, 1, 2));
       if (rec_q)
-        RJ_HIP(hipMemcpyAsync(w->recq, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s1));
+        RJ_HIP(hipMemcpy2DAsync(w->recq, (size_t)W * 8, w->Q0, (size_t)W * 8, (size_t)wr * 8,
+                                (size_t)n, hipMemcpyDeviceToHost, s1));
       if (rec_p)
-        RJ_HIP(hipMemcpyAsync(w->recp, w->Ps, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s1));
+        RJ_HIP(hipMemcpy2DAsync(w->recp, (size_t)W * 8, w->Ps, (size_t)W * 8, (size_t)wr * 8,
+                                (size_t)n, hipMemcpyDeviceToHost, s1));
     }
     const bool reuse = V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta;
     if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order, kIdxV0));
@@ -1116,18 +1142,22 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     for (int64_t c = 0; c < n; ++c)
       if (R.ch[c].move != 0) jump.push_back(c);
     const int64_t nj = (int64_t)jump.size();
+    // a jumping row's columns: its 3 K stars and the one a birth / split adds
+    int32_t kj = 1;
+    for (int64_t c : jump) kj = std::max(kj, Kc[c]);
+    const int64_t dj = std::min<int64_t>(W, 3 * (int64_t)kj + 3);
     double* Jq = w->J;
     double* Jp = w->J + n * W;
     int64_t* jd = D.idx_d(kIdxJump);
     if (nj > 0) {
       std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
       RJ_HIP(hipMemcpyAsync(jd, D.idx_h(kIdxJump), (size_t)nj * 8, hipMemcpyHostToDevice, s0));
-      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, W, nullptr, nj, (int32_t)W, s0))
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
-      if (int rc = rhmc_rows_copy_device(ctx, w->P, W, jd, Jp, W, nullptr, nj, (int32_t)W, s0))
+      if (int rc = rhmc_rows_copy_device(ctx, w->P, W, jd, Jp, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
-      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(nj * W) * 8, hipMemcpyDeviceToHost, s0));
-      RJ_HIP(hipMemcpyAsync(w->Jh + n * W, Jp, (size_t)(nj * W) * 8, hipMemcpyDeviceToHost, s0));
+      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(nj * dj) * 8, hipMemcpyDeviceToHost, s0));
+      RJ_HIP(hipMemcpyAsync(w->Jh + n * W, Jp, (size_t)(nj * dj) * 8, hipMemcpyDeviceToHost, s0));
     }
     RJ_HIP(hipStreamSynchronize(s0));
     lap(2);
@@ -1135,8 +1165,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     for (int64_t j = 0; j < nj; ++j) jpos[j] = j;
     R.parallel(jpos, [&](int64_t j) {
       Chain& h = R.ch[jump[j]];
-      double* rq = w->Jh + j * W;
-      double* rp = w->Jh + n * W + j * W;
+      double* rq = w->Jh + j * dj;
+      double* rp = w->Jh + n * W + j * dj;
       const int64_t d = 3 * (int64_t)h.K;
       h.q.assign(rq, rq + d);
       h.p.resize((size_t)d);
@@ -1147,8 +1177,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
         h.K = h.K0;
         return;  // its rows are restored from Q0 at the accept step
       }
-      std::fill(std::copy(h.q.begin(), h.q.end(), rq), rq + W, 0.);
-      std::fill(std::copy(h.p.begin(), h.p.end(), rp), rp + W, 0.);
+      std::fill(std::copy(h.q.begin(), h.q.end(), rq), rq + dj, 0.);
+      std::fill(std::copy(h.p.begin(), h.p.end(), rp), rp + dj, 0.);
     });
     live.clear();
     for (int64_t c : jump)
@@ -1156,11 +1186,11 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     for (int64_t c : live) Kc[c] = R.ch[c].K;
     lap(3);
     if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
-      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(nj * W) * 8, hipMemcpyHostToDevice, s0));
-      RJ_HIP(hipMemcpyAsync(Jp, w->Jh + n * W, (size_t)(nj * W) * 8, hipMemcpyHostToDevice, s0));
-      if (int rc = rhmc_rows_copy_device(ctx, Jq, W, nullptr, w->Q, W, jd, nj, (int32_t)W, s0))
+      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(nj * dj) * 8, hipMemcpyHostToDevice, s0));
+      RJ_HIP(hipMemcpyAsync(Jp, w->Jh + n * W, (size_t)(nj * dj) * 8, hipMemcpyHostToDevice, s0));
+      if (int rc = rhmc_rows_copy_device(ctx, Jq, dj, nullptr, w->Q, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
-      if (int rc = rhmc_rows_copy_device(ctx, Jp, W, nullptr, w->P, W, jd, nj, (int32_t)W, s0))
+      if (int rc = rhmc_rows_copy_device(ctx, Jp, dj, nullptr, w->P, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
       RJ_TRY(D.upload_K());
     }
@@ -1205,17 +1235,22 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       }
     });
     acc_rows.clear();
+    int32_t kacc = 1;  // an accepted row's columns: its old and new stars
     for (int64_t c = 0; c < n; ++c) {
+      if (acc[c]) {
+        acc_rows.push_back(c);
+        kacc = std::max(kacc, std::max(R.ch[c].K0, R.ch[c].K));
+      }
       Kc[c] = R.ch[c].K;
-      if (acc[c]) acc_rows.push_back(c);
     }
     if (!acc_rows.empty()) {
+      const int64_t dc = std::min<int64_t>(W, 3 * (int64_t)kacc);
       int64_t* cd = D.idx_d(kIdxCommit);
       std::copy(acc_rows.begin(), acc_rows.end(), D.idx_h(kIdxCommit));
       RJ_HIP(hipMemcpyAsync(cd, D.idx_h(kIdxCommit), acc_rows.size() * 8, hipMemcpyHostToDevice,
                             s0));
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, cd, w->Q0, W, cd,
-                                         (int64_t)acc_rows.size(), (int32_t)W, s0))
+                                         (int64_t)acc_rows.size(), (int32_t)dc, s0))
         return D.engine_fail(rc, "commit");
     }
     lap(6);
@@ -1372,6 +1407,29 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
     });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
+  } catch (const std::exception& e) {
+    return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
+  }
+}
+
+int rhmc_rj_release(int32_t device) {
+  try {
+    DeviceGuard guard;
+    std::lock_guard<std::mutex> lock(g_work_mu);
+    for (auto it = g_work.begin(); it != g_work.end();) {
+      if (device >= 0 && it->first.first != device) {
+        ++it;
+        continue;
+      }
+      Work* w = it->second;
+      {
+        std::lock_guard<std::mutex> l(w->mu);  // a run using it finishes first
+        w->destroy();
+      }
+      delete w;
+      it = g_work.erase(it);
+    }
+    return 0;
   } catch (const std::exception& e) {
     return fail(RHMC_ERR_NOMEM, std::string("host exception: ") + e.what());
   }

@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so")
 DEAD_END = 1                 # RHMC_RJ_DEAD_END
 
 EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_beta_eval",
-           "rhmc_rj_pack_starts", "rhmc_rj_last_error")
+           "rhmc_rj_pack_starts", "rhmc_rj_release", "rhmc_rj_last_error")
 
 ENERGY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
                              ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int32,
@@ -92,6 +92,7 @@ def _load():
                           ctypes.c_int64, vp],
         "rhmc_rj_beta_eval": [ctypes.c_double, ctypes.c_double, vp, ctypes.c_int64, vp, vp],
         "rhmc_rj_pack_starts": [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, vp],
+        "rhmc_rj_release": [ctypes.c_int32],
     }
     for name, args in sig.items():
         fn = getattr(lib, name)
@@ -112,6 +113,12 @@ def lib():
 def _check(rc):
     if rc != capi.RHMC_OK:
         raise capi.RhmcError(rc, _lib.rhmc_rj_last_error().decode(errors="replace"))
+
+
+def release(device=-1):
+    """Free the device and pinned buffers the driver keeps between runs
+    (rhmc_rj_release; device < 0: every device)."""
+    _check(_lib.rhmc_rj_release(int(device)))
 
 
 def np_draws(seed, kind, n, a=0., b=0.):

@@ -684,7 +684,8 @@ class multi_gym(base_class):
     def run_RHMC_rj_batched(self, q_models_0, seeds, f_pos=True, delta=1e-6, Niter=100,
                             Nsteps=100, dt=1e-1, counter_max=1000, N_max=50,
                             P_move=[1., 0., 0.], schedule_g_ff2=None, schedule_beta=None,
-                            engine="native", n_threads=0, n_pipes=0, rng_states=None):
+                            engine="native", n_threads=0, n_pipes=0, rng_states=None,
+                            reuse_records=False):
         """Many independent chains of run_RHMC WITH the reversible-jump moves
         (sampler_RHMC.py:937-1198; birth_death_move :1200-1270, split_merge_move
         :1273-1445), each chain at its own, changing, star count.  Chain c is
@@ -727,7 +728,7 @@ class multi_gym(base_class):
                 raise ValueError("one seed per chain")
             return self._rj_native(q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt,
                                    counter_max, N_max, P_move, schedule_g_ff2, schedule_beta,
-                                   n_threads, n_pipes, rng_states)
+                                   n_threads, n_pipes, rng_states, reuse_records)
         if engine != "python":
             raise ValueError("engine must be 'native' or 'python'")
         if rng_states is not None:
@@ -853,7 +854,7 @@ class multi_gym(base_class):
 
     def _rj_native(self, q_models_0, seeds, f_pos, delta, Niter, Nsteps, dt, counter_max, N_max,
                    P_move, schedule_g_ff2, schedule_beta, n_threads, n_pipes=0,
-                   rng_states=None):
+                   rng_states=None, reuse_records=False):
         """run_RHMC_rj_batched through librhmc_rj.so (rhmc_rj_run)."""
         from . import rj_native
         self._check_geometry()
@@ -878,15 +879,18 @@ class multi_gym(base_class):
         else:
             packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max)
         P = self._params(delta, counter_max, for_energy=True)
-        # the previous run's q_chain / p_chain memory takes this run's records
-        # when nothing but this sampler holds it (no caller reference, no view:
-        # the attribute, `a` and getrefcount's argument) — fresh arrays of this
-        # size cost a page fault per 4 KiB inside the run
+        # reuse_records (opt-in): the previous run's q_chain / p_chain memory
+        # takes this run's records when nothing but this sampler holds it (no
+        # caller reference, no view: the attribute, `a` and getrefcount's
+        # argument) — fresh arrays of this size cost a page fault per 4 KiB
+        # inside the run.  The attributes are detached until the run succeeds,
+        # so a failed run leaves None, not half-overwritten records.
         out = {}
-        for key in ("q_chain", "p_chain"):
+        for key in (("q_chain", "p_chain") if reuse_records else ()):
             a = self.__dict__.get(key)
             if isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3:
                 out[key] = a
+                setattr(self, key, None)
             a = None
         import time
         t0 = time.perf_counter()

@@ -63,9 +63,16 @@
  *   - Every call returns 0 on success or a negative RHMC_ERR_* code;
  *     rhmc_last_error() gives a thread-local message.  No C++ exception
  *     crosses the ABI.  A context must not be used by two threads at once,
- *     except that rhmc_leapfrog_device and rhmc_energy_device (whose only
- *     state in the context is a per-stream, mutex-guarded table buffer) may be
- *     called from several threads on distinct streams; one context per GPU.
+ *     except that rhmc_leapfrog_device, rhmc_energy_device,
+ *     rhmc_leapfrog_ragged_device, rhmc_energy_ragged_device,
+ *     rhmc_rows_copy_device, rhmc_kinetic_rows_device and rhmc_ragged_ok
+ *     (which read the context's options and image and otherwise touch only a
+ *     per-stream, mutex-guarded table buffer) may be called from several
+ *     threads at once, on the same or distinct streams: a launch holds a
+ *     reference to the table buffer it was given until it is enqueued, so a
+ *     buffer grown by another thread is released only after that launch (the
+ *     order of two threads' launches on one stream is theirs to arrange).
+ *     Options must not change while such calls run.  One context per GPU.
  */
 #ifndef RHMC_H
 #define RHMC_H
@@ -164,11 +171,30 @@ typedef struct rhmc_ctx rhmc_ctx;
  *   than 64 px, or K > 16); the factor-table variant, the explicit solvers,
  *   HMC_random and every other kernel family ignore it, and
  *   rhmc_ctx_get_option returns the value set either way.
+ * RHMC_OPT_TABLES (diagnostic; results do not depend on it): where the
+ *   windowed kernels from 65 stars keep their per-chain PSF factor tables in
+ *   global memory.  STREAM (default) = one buffer per (context, stream);
+ *   STREAM_POISON = the same, filled with 0xFF bytes (NaN) before every
+ *   launch, so a read of an entry the launch did not write would show as a
+ *   NaN result; POOL / POOL_POISON = one stream-ordered pool allocation per
+ *   launch (hipMallocAsync / hipFreeAsync behind it), without / with the fill;
+ *   POOL_KEEP = a pool allocation per launch that is never reused (released
+ *   at rhmc_ctx_destroy); POOL_SYNCFREE = a pool allocation per launch,
+ *   released after a sync of the launch's stream.
  */
 enum {
   RHMC_OPT_KERNEL = 1,
   RHMC_OPT_MH_FUSED = 2,
-  RHMC_OPT_WINDOW_SPLIT = 3
+  RHMC_OPT_WINDOW_SPLIT = 3,
+  RHMC_OPT_TABLES = 4
+};
+enum {
+  RHMC_TABLES_STREAM = 0,
+  RHMC_TABLES_STREAM_POISON = 1,
+  RHMC_TABLES_POOL = 2,
+  RHMC_TABLES_POOL_POISON = 3,
+  RHMC_TABLES_POOL_KEEP = 4,
+  RHMC_TABLES_POOL_SYNCFREE = 5
 };
 enum {
   RHMC_KERNEL_AUTO = 0,

@@ -30,10 +30,17 @@
  * caller-supplied engine callbacks (stand-ins for tests), one call per
  * distinct star count and phase.
  *
- * Concurrency: each pipe of a run uses process-lifetime device buffers and two
- * HIP streams of its own, held (a mutex) for the whole run, so concurrent
- * rhmc_rj_run calls on one device serialise pipe by pipe; the caller's
- * current device is restored on return.
+ * Concurrency: each pipe of a run uses device buffers and two HIP streams of
+ * its own, held (a mutex) for the whole run, so concurrent rhmc_rj_run calls
+ * on one device serialise pipe by pipe; the caller's current device is
+ * restored on return.
+ *
+ * Retention: those buffers (per device and pipe index, grown to the largest
+ * run so far: ~90 MB of HBM and ~60 MB of pinned host memory per pipe at
+ * 4,096 chains and N_max 120, 8 pipes from 16,384 chains) stay allocated
+ * after a run, so the next run starts without allocating;
+ * rhmc_rj_release(device) frees them (device < 0: every device), waiting for
+ * a run that holds one.
  *
  * Replaces: the per-chain Python loop of run_RHMC's reversible-jump branches
  * (one chain, one star count at a time) — this is its batched, native form.
@@ -157,6 +164,11 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
 int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
                         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds,
                         int64_t n, const rhmc_rj_record* rec);
+
+/* Free the buffers, streams and events rhmc_rj_run keeps between runs (see
+ * Retention above) on `device`, or on every device when device < 0.  A later
+ * run allocates them again.  Not to be called from inside a physics callback. */
+int rhmc_rj_release(int32_t device);
 
 /* The NumPy legacy stream replica, for parity checks: n draws from
  * RandomState(seed) of `kind` into out.  kind 0: random_sample(); 1: randn();

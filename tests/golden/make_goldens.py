@@ -777,7 +777,7 @@ def case_rj_big(S, U):
     return {"rj_big": out}
 
 
-def case_flagship(S, U):
+def case_flagship(S, U, niter=40, compact=False):
     """The reference's flagship run, RHMC-big-sim4.py, as written except
     Niter (40 instead of 10000) and verbose (off: it only prints and plots,
     which draws nothing from the RNG): seed 77, 32x32, 51 true stars from the
@@ -823,11 +823,26 @@ def case_flagship(S, U):
     finally:
         np.histogram = orig_hist
     st_run = np.random.get_state()
-    niter, nsteps, dt, N_max, P_move = 40, 10, 5e-2, 120, [0.6, 0.2, 0.2]
+    nsteps, dt, N_max, P_move = 10, 5e-2, 120, [0.6, 0.2, 0.2]
     with contextlib.redirect_stdout(io.StringIO()):
         g.run_RHMC(q_model.copy(), f_pos=True, delta=1e-6, Niter=niter, Nsteps=nsteps,
                    dt=dt, save_traj=False, verbose=False, q_true=q_true,
                    schedule_beta=None, P_move=P_move, N_max=N_max)
+    if compact:  # the written length: records that say where two runs part
+        res = dict(D=g.D, q_true=q_true, q_model=q_model,
+                   rng_key=st_run[1], rng_pos=st_run[2],
+                   rng_gauss=np.array([st_run[3], st_run[4]]),
+                   E_chain=g.E_chain, V_chain=g.V_chain, T_chain=g.T_chain,
+                   A_chain=g.A_chain.astype(np.int32), move_chain=g.move_chain,
+                   N_chain=g.N_chain, q_every100=g.q_chain[::100], P_move=np.array(P_move),
+                   niter=niter, nsteps=nsteps, dt=dt, N_max=N_max,
+                   K_split=g.K_split, beta_a=g.beta_a, beta_b=g.beta_b)
+        out = pack("", res)
+        out.update(pack("par_", gym_params(g)))
+        print("flagship_long moves", np.bincount(g.move_chain, minlength=5),
+              "accepted", np.bincount(g.move_chain[g.A_chain], minlength=5),
+              "N", g.N_chain.min(), g.N_chain.max())
+        return {"flagship_long": out}
     res = dict(D=g.D, q_true=q_true, q_model=q_model,
                rng_data_key=st_data[1], rng_data_pos=st_data[2],
                rng_data_gauss=np.array([st_data[3], st_data[4]]),
@@ -925,6 +940,10 @@ def main():
             np.savez_compressed(os.path.join(HERE, "mh_bigk.npz"), **case_mh_bigk(S, U))
             print("wrote mh_bigk")
         # subsets of the above, regenerated on their own (--only c5 / bigk)
+        if args.only == "flagship_long":   # RHMC-big-sim4.py at Niter = 10000 (minutes)
+            for name, d in case_flagship(S, U, niter=10000, compact=True).items():
+                np.savez_compressed(os.path.join(HERE, name + ".npz"), **d)
+                print("wrote", name)
         for job, fn in (("c5", case_c5), ("bigk", case_bigk), ("flagship", case_flagship),
                         ("rj_big", case_rj_big), ("hugek", case_hugek)):
             if args.only == job or (not args.only and job in ("bigk", "flagship", "rj_big",

@@ -185,10 +185,12 @@ def test_native_across_256_stars(gpu_lib):
 
 
 def test_native_record_buffers_reused_only_when_unreferenced(gpu_lib):
-    """A second run writes its q_chain / p_chain records into the first run's
-    memory only when nothing but the sampler holds it; the records equal a
-    fresh sampler's either way (every row, padding included, is overwritten),
-    and a caller's reference keeps the first run's records intact."""
+    """With reuse_records=True (opt-in: bench.py) a second run writes its
+    q_chain / p_chain records into the first run's memory only when nothing
+    but the sampler holds it; the records equal a fresh sampler's either way
+    (every row, padding included, is overwritten), and a caller's reference
+    keeps the first run's records intact.  Without the flag a run never
+    reuses them."""
     z = load_golden("rj")
     name = "rj_all"
     par = R.params_from_npz(z, name + "/par_")
@@ -199,8 +201,16 @@ def test_native_record_buffers_reused_only_when_unreferenced(gpu_lib):
         return g
     starts = _starts(z[name + "/q_model"], 24, np.random.RandomState(3))
     kw = dict(f_pos=True, delta=1e-6, Niter=5, Nsteps=4, dt=0.05, N_max=12,
-              P_move=[0.4, 0.3, 0.3])
+              P_move=[0.4, 0.3, 0.3], reuse_records=True)
     g = make()
+    g.run_RHMC_rj_batched(starts, list(range(24)), **kw)
+    first = g.q_chain.copy()
+    addr = g.q_chain.ctypes.data
+    held = g.q_chain
+    g.run_RHMC_rj_batched(starts, list(range(24)), **dict(kw, reuse_records=False))
+    assert g.q_chain is not held and g.q_chain.ctypes.data != addr   # not opted in
+    np.testing.assert_array_equal(g.q_chain, first)
+    held = None
     g.run_RHMC_rj_batched(starts, list(range(24)), **kw)
     first = g.q_chain.copy()
     addr = g.q_chain.ctypes.data

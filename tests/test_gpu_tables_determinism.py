@@ -123,3 +123,117 @@ def test_windowed_global_tables_two_threads(gpu_lib):
         assert np.array_equal(q.cpu().numpy(), serial[0].cpu().numpy())
         assert np.array_equal(p.cpu().numpy(), serial[1].cpu().numpy())
     ctx.close()
+
+
+def _all_paths(capi, mode, wl, n):
+    """Leapfrog (status, iteration counts), energy V / T and the MH loop on the
+    global-table path, on a fresh context in table mode `mode`."""
+    import torch
+    dev = torch.device("cuda", 0)
+    P = capi.make_params(**wl.params)
+    ctx = capi.Context(wl.D)
+    ctx.set_option(capi.OPT_TABLES, mode)
+    assert ctx.get_option(capi.OPT_TABLES) == mode
+    q = torch.from_numpy(np.ascontiguousarray(wl.q0[:n])).to(dev)
+    p = torch.from_numpy(np.ascontiguousarray(wl.p0[:n])).to(dev)
+    it = torch.zeros((n, 2), dtype=torch.int32, device=dev)
+    st = torch.zeros(n, dtype=torch.int32, device=dev)
+    V = torch.zeros(n, dtype=torch.float64, device=dev)
+    T = torch.zeros(n, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(2):
+        ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), n, wl.K, 3, it.data_ptr(),
+                            st.data_ptr())
+    ctx.energy_device(P, q.data_ptr(), p.data_ptr(), V.data_ptr(), T.data_ptr(), n, wl.K)
+    torch.cuda.synchronize()
+    out = [x.cpu().numpy() for x in (q, p, it, st, V, T)]
+    s = torch.cuda.Stream(dev)
+    out += list(_mh(capi, ctx, P, wl, wl.q0, n, s, n_iter=3, leap=6))
+    ctx.close()
+    return out
+
+
+def test_global_tables_poisoned_equal_unpoisoned(gpu_lib):
+    """every table entry a launch reads, it wrote in that
+    launch.  RHMC_OPT_TABLES fills the buffer with 0xFF bytes (NaN doubles)
+    before every launch (STREAM_POISON), or takes a fresh stream-ordered pool
+    allocation per launch with (POOL_POISON) or without the fill (POOL, round
+    5's first scheme): leapfrog, energy and MH must equal the default buffer
+    bit for bit, with no chain non-finite."""
+    capi = gpu_lib
+    wl = workloads.make("S256K100", n_chains=512)
+    base = _all_paths(capi, capi.TABLES_STREAM, wl, wl.n_chains)
+    q, p, it, st, V, T, qm, acc = base
+    assert not (st & capi.STATUS_NONFINITE).any()
+    # (V is inf for a chain with a star off the image: the position support, :303-317)
+    assert np.isfinite(V).mean() > 0.5 and np.isfinite(T).all() and np.isfinite(qm).all()
+    assert 0.0 < acc.mean() < 1.0
+    for mode in (capi.TABLES_STREAM_POISON, capi.TABLES_POOL, capi.TABLES_POOL_POISON):
+        got = _all_paths(capi, mode, wl, wl.n_chains)
+        for a, b, name in zip(got, base, ("q", "p", "iters", "status", "V", "T", "q_mh", "acc")):
+            assert np.array_equal(a, b), (mode, name)
+
+
+@pytest.mark.parametrize("Ks", [[65, 90, 70, 128, 88, 77, 66], [300, 257, 400]])
+def test_global_tables_poisoned_ragged_and_hugek(gpu_lib, Ks):
+    """The ragged launches (tables laid out by the launch's K_max, each chain
+    reading its own K's entries) and the 8-slot kernels past 256 stars under
+    the NaN fill equal the unfilled buffer bit for bit."""
+    import torch
+    capi = gpu_lib
+    from helpers import capi_params
+    from conftest import load_golden
+    from oracle import rhmc_ref as R
+    z = load_golden("traj_bigk256" if max(Ks) <= 128 else "traj_hugek")
+    D, par = z["D"], R.params_from_npz(z)
+    rs = np.random.RandomState(11)
+    ld = 3 * max(Ks)
+    n_pix = D.shape[0]
+    m = R.RefModel(np.zeros((n_pix, n_pix)), par)
+    q = np.zeros((len(Ks), ld))
+    p = np.zeros((len(Ks), ld))
+    for c, K in enumerate(Ks):
+        row = np.stack([par["f_lim"] * np.exp(1 + 2 * rs.rand(K)), 1 + (n_pix - 2) * rs.rand(K),
+                        1 + (n_pix - 2) * rs.rand(K)], 1).reshape(-1)
+        q[c, :3 * K] = row
+        p[c, :3 * K] = rs.randn(3 * K) * np.sqrt(m.H(row))
+    dev = torch.device("cuda:0")
+    res = []
+    for mode in (capi.TABLES_STREAM, capi.TABLES_STREAM_POISON, capi.TABLES_POOL_POISON):
+        ctx = capi.Context(D)
+        ctx.set_option(capi.OPT_TABLES, mode)
+        P = capi_params(capi, par)
+        qd = torch.from_numpy(q.copy()).to(dev)
+        pd = torch.from_numpy(p.copy()).to(dev)
+        Kd = torch.tensor(Ks, dtype=torch.int32, device=dev)
+        rows = torch.arange(len(Ks), dtype=torch.int64, device=dev)
+        Vd = torch.zeros(len(Ks), dtype=torch.float64, device=dev)
+        torch.cuda.synchronize()
+        if max(Ks) <= 128:
+            lo, hi = min(Ks), max(Ks)
+            ctx.energy_ragged_device(P, qd.data_ptr(), ld, rows.data_ptr(), Kd.data_ptr(),
+                                     len(Ks), lo, hi, capi.V_FLUX_WALL, Vd.data_ptr())
+            ctx.leapfrog_ragged_device(P, qd.data_ptr(), pd.data_ptr(), ld, rows.data_ptr(),
+                                       Kd.data_ptr(), len(Ks), lo, hi, 2)
+            torch.cuda.synchronize()
+            res.append((qd.cpu().numpy(), pd.cpu().numpy(), Vd.cpu().numpy()))
+        else:   # fixed-K launches, one chain each (8 register slots)
+            out = []
+            for c, K in enumerate(Ks):
+                V, T = ctx.energy(P, q[c, :3 * K][None], p[c, :3 * K][None], f_pos=True)
+                g = ctx.gradient(P, q[c, :3 * K][None], kind=1)
+                q1, p1, it, st = ctx.leapfrog(P, q[c, :3 * K][None], p[c, :3 * K][None], 1,
+                                              return_info=True)
+                assert not (st & capi.STATUS_NONFINITE).any()
+                out.append((V, T, g, q1, p1, it))
+            res.append(out)
+        ctx.close()
+    for r in res[1:]:
+        if max(Ks) <= 128:
+            for a, b in zip(r, res[0]):
+                assert np.array_equal(a, b)
+            assert np.isfinite(res[0][2]).all()
+        else:
+            for ca, cb in zip(r, res[0]):
+                for a, b in zip(ca, cb):
+                    assert np.array_equal(a, b)
