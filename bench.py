@@ -447,11 +447,12 @@ def main():
     ap.add_argument("--window-split", type=int, choices=(0, 1, 2, 4), default=0,
                     help="RHMC_OPT_WINDOW_SPLIT for the multi-star register-window kernel "
                          "(0: by batch size; results bit-identical)")
-    ap.add_argument("--tables", type=int, choices=(0, 1, 2, 3, 4, 5), default=0,
+    ap.add_argument("--tables", type=int, choices=(0, 1, 2, 3, 4, 5, 6), default=0,
                     help="RHMC_OPT_TABLES (diagnostic): 0 per-stream buffer, 1 the same "
                          "NaN-filled before each launch, 2 / 3 per-launch pool allocation "
                          "without / with the fill, 4 pool allocation never reused, 5 pool "
-                         "allocation freed after a stream sync")
+                         "allocation freed after a stream sync, 6 pool allocation behind an "
+                         "event barrier")
     ap.add_argument("--solver", choices=("hmc", "naive", "leap_frog"), default="leap_frog")
     ap.add_argument("--n-real", type=int, default=1000)
     ap.add_argument("--dry-run", action="store_true",
@@ -677,6 +678,23 @@ def main():
     }
     if args.mode == "leapfrog" and not args.no_e2e and world == 1:
         out["end_to_end"] = end_to_end(ctx, P, q, p, wl, leap)
+    if args.tables:
+        out["config"]["tables"] = args.tables
+        # a -DRHMC_TABLE_CANARY diagnostic library (tools/table_canary.py) also
+        # reports the table regions other work wrote into during a gradient
+        fn = getattr(capi.lib(), "rhmc_debug_table_conflicts", None)
+        if fn is not None:
+            import ctypes
+            c3 = (ctypes.c_int64 * 5)()
+            fn.argtypes = [ctypes.POINTER(ctypes.c_int64)]
+            fn(c3)
+            out["table_conflicts"] = list(c3)
+            seen = (ctypes.c_uint64 * 9)()
+            capi.lib().rhmc_debug_table_seen(seen)
+            import struct
+            out["table_foreign_values"] = [
+                {"hex": "%016x" % v, "as_f64": struct.unpack("<d", struct.pack("<Q", v))[0]}
+                for v in list(seen)[1:1 + min(8, seen[0])]]
     if rank == 0:
         out["cpu_baseline"] = cpu
         print(json.dumps(out), flush=True)

@@ -1133,7 +1133,8 @@ int work_tables(const rhmc_ctx* ctx, int path, int K, int64_t n, hipStream_t st,
   const int mode = ctx->table_mode;
   const bool poison = mode == RHMC_TABLES_STREAM_POISON || mode == RHMC_TABLES_POOL_POISON;
   if (mode == RHMC_TABLES_POOL || mode == RHMC_TABLES_POOL_POISON ||
-      mode == RHMC_TABLES_POOL_KEEP || mode == RHMC_TABLES_POOL_SYNCFREE) {
+      mode == RHMC_TABLES_POOL_KEEP || mode == RHMC_TABLES_POOL_SYNCFREE ||
+      mode == RHMC_TABLES_POOL_BARRIER) {
     // Diagnostic: round 5's first scheme, one stream-ordered pool allocation
     // per launch, released behind it (~TabBuf: hipFreeAsync on st).
     auto b = std::make_shared<rhmc_ctx::TabBuf>();
@@ -1147,6 +1148,13 @@ int work_tables(const rhmc_ctx* ctx, int path, int K, int64_t n, hipStream_t st,
     }
     b->bytes = bytes;
     if (poison) HIP_TRY(hipMemsetAsync(b->p, 0xFF, bytes, st));
+    if (mode == RHMC_TABLES_POOL_BARRIER) {  // the launch waits for everything before it
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(e, st));
+      HIP_TRY(hipStreamWaitEvent(st, e, 0));
+      HIP_TRY(hipEventDestroy(e));
+    }
     *out = (double*)b->p;
     if (mode == RHMC_TABLES_POOL_KEEP) {  // never reused: released at rhmc_ctx_destroy
       std::lock_guard<std::mutex> lk(ctx->tab_mu);
@@ -2655,8 +2663,16 @@ int rhmc_ctx_set_option(rhmc_ctx* ctx, int32_t option, int32_t value) {
       ctx->window_split = value;
       return RHMC_OK;
     case RHMC_OPT_TABLES:
-      if (value < RHMC_TABLES_STREAM || value > RHMC_TABLES_POOL_SYNCFREE)
-        return fail(RHMC_ERR_ARG, "RHMC_OPT_TABLES must be 0 ... 5");
+      if (value < RHMC_TABLES_STREAM || value > RHMC_TABLES_POOL_BARRIER)
+        return fail(RHMC_ERR_ARG, "RHMC_OPT_TABLES must be 0 ... 6");
+#ifndef RHMC_TABLE_DIAG
+      // the stream-ordered pool modes reproduce a runtime defect (DESIGN.md
+      // section 4a: reused blocks are zeroed under a running launch); only
+      // diagnostic builds take them
+      if (value > RHMC_TABLES_STREAM_POISON)
+        return fail(RHMC_ERR_UNSUPPORTED,
+                    "RHMC_OPT_TABLES pool modes exist only in -DRHMC_TABLE_DIAG builds");
+#endif
       ctx->table_mode = value;
       return RHMC_OK;
     default:
@@ -3145,14 +3161,22 @@ int rhmc_gen_image(rhmc_ctx* ctx, const rhmc_params* P, const double* q, int32_t
 
 #ifdef RHMC_TABLE_CANARY
 // Diagnostic builds only (not declared in rhmc.h): the table-region conflicts
-// seen since the last call, [total, in gradients, in potentials]; resets them.
-int rhmc_debug_table_conflicts(int64_t* out3) {
-  unsigned long long h[3] = {0, 0, 0};
+// seen since the last call (rhmc_windowed.hpp canary_leave: calls that saw a
+// bump, gradients / potentials that saw one, gradient / potential bumps
+// seen); resets them.
+int rhmc_debug_table_conflicts(int64_t* out5) {
+  unsigned long long h[6] = {0, 0, 0, 0, 0, 0};
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_tab_conflicts), sizeof(h)));
-  const unsigned long long z[3] = {0, 0, 0};
+  const unsigned long long z[6] = {0, 0, 0, 0, 0, 0};
   HIP_TRY(hipMemcpyToSymbol(HIP_SYMBOL(g_tab_conflicts), z, sizeof(z)));
-  for (int i = 0; i < 3; ++i) out3[i] = (int64_t)h[i];
+  for (int i = 0; i < 5; ++i) out5[i] = (int64_t)h[i];
+  return RHMC_OK;
+}
+// The first 8 foreign header values a canary saw (raw 64-bit), [0] = how many.
+int rhmc_debug_table_seen(uint64_t* out9) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(out9, HIP_SYMBOL(g_tab_seen), 9 * sizeof(uint64_t)));
   return RHMC_OK;
 }
 #endif

@@ -59,40 +59,48 @@ __device__ __forceinline__ int readlane_i(int v, int src) {
 template <bool GT>
 __device__ __forceinline__ void tab_sync() {
   if constexpr (GT) {
-#ifdef RHMC_GT_FENCE_AGENT  // diagnostic build: agent scope (L1 written back / invalidated)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#else
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-#endif
   } else {
     wave_lds_sync();
   }
 }
 
 // Diagnostic build (-DRHMC_TABLE_CANARY, never the product library): each
-// wave's global table region starts with a 64-bit counter that lane 0 bumps
-// when a gradient / potential starts and again when it ends; a bump by
-// anything else in between (another launch using the same region) is counted
-// in g_tab_conflicts, tagged by the kind of call that saw it (1 gradient,
-// 2 potential), and read by rhmc_debug_table_conflicts().
+// wave's global table region starts with a 64-bit counter to which lane 0 adds
+// the call's tag when a gradient (tag 1) or potential (tag 2^32) starts and
+// again when it ends; anything else that bumped it in between (another call
+// in the same region at the same time) is counted in g_tab_conflicts:
+// [0] calls that saw a bump, [1] / [2] gradients / potentials that saw one,
+// [3] / [4] the gradient / potential bumps they saw (enter + leave of every
+// foreign call); rhmc_debug_table_conflicts() reads them.  Other writers
+// (not tagged) show as a bump of neither kind.
 #ifdef RHMC_TABLE_CANARY
+#ifndef RHMC_TABLE_DIAG
+#define RHMC_TABLE_DIAG 1  // the pool modes of RHMC_OPT_TABLES
+#endif
 constexpr int kTabHeader = 8;  // doubles before a wave's tables
-__device__ unsigned long long g_tab_conflicts[3];
-__device__ __forceinline__ unsigned long long canary_enter(double* hdr) {
+__device__ unsigned long long g_tab_conflicts[6];
+__device__ unsigned long long g_tab_seen[9];  // [0] count, then the first 8 foreign header values
+__device__ __forceinline__ unsigned long long canary_enter(double* hdr, int kind) {
   unsigned long long v = 0;
-  if (lane_id() == 0) v = atomicAdd((unsigned long long*)hdr, 1ull);
+  const unsigned long long tag = kind == 1 ? 1ull : (1ull << 32);
+  if (lane_id() == 0) v = atomicAdd((unsigned long long*)hdr, tag);
   return v;
 }
 __device__ __forceinline__ void canary_leave(double* hdr, unsigned long long v, int kind) {
   if (lane_id() == 0) {
-    const unsigned long long now = atomicAdd((unsigned long long*)hdr, 1ull);
-    if (now != v + 1ull) {
+    const unsigned long long tag = kind == 1 ? 1ull : (1ull << 32);
+    const unsigned long long now = atomicAdd((unsigned long long*)hdr, tag);
+    if (now != v + tag) {
+      const unsigned long long d = now - (v + tag);
       atomicAdd(&g_tab_conflicts[0], 1ull);
       atomicAdd(&g_tab_conflicts[kind], 1ull);
+      atomicAdd(&g_tab_conflicts[3], d & 0xffffffffull);
+      atomicAdd(&g_tab_conflicts[4], d >> 32);
+      const unsigned long long slot = atomicAdd(&g_tab_seen[0], 1ull);
+      if (slot < 8ull) atomicExch(&g_tab_seen[1 + slot], now);
     }
   }
 }
@@ -181,7 +189,7 @@ __device__ void win_gradient(const double* __restrict__ D, const WinTables& t, i
                              double (&gx)[SLOTS], double (&gy)[SLOTS]) {
   const int lane = lane_id();
 #ifdef RHMC_TABLE_CANARY
-  const unsigned long long cv = GT ? canary_enter(t.ex - kTabHeader) : 0ull;
+  const unsigned long long cv = GT ? canary_enter(t.ex - kTabHeader, 1) : 0ull;
 #endif
   int bx[SLOTS], by[SLOTS];
 #pragma unroll
@@ -368,7 +376,7 @@ __device__ double win_potential(const double* __restrict__ D, double* ey,
   constexpr int R = kPotRows;
   const int lane = lane_id();
 #ifdef RHMC_TABLE_CANARY
-  const unsigned long long cv = GT ? canary_enter(ey - kTabHeader) : 0ull;
+  const unsigned long long cv = GT ? canary_enter(ey - kTabHeader, 2) : 0ull;
 #endif
   int bx[SLOTS], by[SLOTS];
 #pragma unroll
@@ -547,11 +555,7 @@ struct WinEG {
 struct WinGG {
   static __host__ __device__ size_t lds_bytes(int, int) { return kExpTab * sizeof(double); }
   static __host__ __device__ size_t work_doubles(int K) {
-#ifdef RHMC_TAB_PAD  // diagnostic: each wave's region on whole 128-byte lines
-    return (win_table_doubles(K) + kTabHeader + 15) / 16 * 16;
-#else
     return win_table_doubles(K) + kTabHeader;
-#endif
   }
   using Ctx = WinG::Ctx;
   static __device__ __forceinline__ Ctx setup(double* lds, const double* D, int K, int rows,

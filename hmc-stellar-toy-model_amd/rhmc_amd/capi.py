@@ -33,7 +33,7 @@ OPT_MH_FUSED = 2
 OPT_WINDOW_SPLIT = 3        # waves per chain pair in leapfrog_kr (0: by batch size)
 OPT_TABLES = 4              # where WinGG keeps its factor tables (diagnostic, rhmc.h)
 (TABLES_STREAM, TABLES_STREAM_POISON, TABLES_POOL, TABLES_POOL_POISON, TABLES_POOL_KEEP,
- TABLES_POOL_SYNCFREE) = range(6)
+ TABLES_POOL_SYNCFREE, TABLES_POOL_BARRIER) = range(7)
 # RHMC_KERNEL_* values by name
 KERNELS = {"auto": 0, "generic": 1, "windowed": 2, "regwin": 3, "regwin32": 4,
            "regwin_f64": 5, "lane1": 6, "lane4": 7, "lane1_f64": 8, "pixmajor": 9,

@@ -171,16 +171,17 @@ typedef struct rhmc_ctx rhmc_ctx;
  *   than 64 px, or K > 16); the factor-table variant, the explicit solvers,
  *   HMC_random and every other kernel family ignore it, and
  *   rhmc_ctx_get_option returns the value set either way.
- * RHMC_OPT_TABLES (diagnostic; results do not depend on it): where the
- *   windowed kernels from 65 stars keep their per-chain PSF factor tables in
- *   global memory.  STREAM (default) = one buffer per (context, stream);
- *   STREAM_POISON = the same, filled with 0xFF bytes (NaN) before every
- *   launch, so a read of an entry the launch did not write would show as a
- *   NaN result; POOL / POOL_POISON = one stream-ordered pool allocation per
- *   launch (hipMallocAsync / hipFreeAsync behind it), without / with the fill;
- *   POOL_KEEP = a pool allocation per launch that is never reused (released
- *   at rhmc_ctx_destroy); POOL_SYNCFREE = a pool allocation per launch,
- *   released after a sync of the launch's stream.
+ * RHMC_OPT_TABLES (diagnostic; results do not depend on it): the windowed
+ *   kernels from 65 stars keep their per-chain PSF factor tables in global
+ *   memory, one buffer per (context, stream).  STREAM (default) = that
+ *   buffer; STREAM_POISON = the same, filled with 0xFF bytes (NaN) before
+ *   every launch, so that a read of an entry the launch did not write would
+ *   show as a NaN result (tests/test_gpu_tables_determinism.py: none does).
+ *   The POOL* values (a stream-ordered pool allocation per launch, round 5's
+ *   first scheme, and its variants) reproduce a defect outside the kernels
+ *   (a reused pool block is zeroed while the launch that
+ *   received it runs); only -DRHMC_TABLE_DIAG builds accept them, the library
+ *   returns RHMC_ERR_UNSUPPORTED.
  */
 enum {
   RHMC_OPT_KERNEL = 1,
@@ -194,7 +195,8 @@ enum {
   RHMC_TABLES_POOL = 2,
   RHMC_TABLES_POOL_POISON = 3,
   RHMC_TABLES_POOL_KEEP = 4,
-  RHMC_TABLES_POOL_SYNCFREE = 5
+  RHMC_TABLES_POOL_SYNCFREE = 5,
+  RHMC_TABLES_POOL_BARRIER = 6
 };
 enum {
   RHMC_KERNEL_AUTO = 0,

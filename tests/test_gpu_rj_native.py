@@ -367,3 +367,46 @@ def test_native_reproduces_reference_goldens(gpu_lib, golden, name):
     np.testing.assert_allclose(g.V_chain[:, 0], z[name + "/V_chain"], rtol=1e-11)
     if golden == "mh_sched":
         assert g.g_ff2 == z[name + "/g_ff2_final"] and g.beta == z[name + "/beta_final"]
+
+
+@pytest.mark.parametrize("case", ["pixk_dense32", "dense_slots32", "kr_wingg64"])
+def test_native_recorded_V_across_family_boundaries(gpu_lib, case):
+    """The V reuse (include/rhmc_rj.h: an iteration's V(q) is the previous
+    iteration's V(q') or V(q)) holds only if a chain's V does not depend on
+    the launch it was evaluated in.  Births, deaths, splits and merges move
+    chains across the kernel families' star-count boundaries, so each
+    boundary is crossed here, and every recorded V must equal the engine's V
+    of that row alone (one chain, fixed K) bit for bit:
+      pixk_dense32  32x32, 8-12 stars: ragged pixel-major (2-10) <-> ragged
+                    dense slot 1 (11-64) — the flagship's range;
+      dense_slots32 32x32, 61-68 stars: dense slot 1 <-> dense slot 2;
+      kr_wingg64    64x64, 61-68 stars: packed multi-star register-window
+                    launches (<= 64) <-> ragged windowed global tables (WinGG,
+                    >= 65)."""
+    zb = load_golden("traj_hugek" if case == "kr_wingg64" else "traj_bigk")
+    par = R.params_from_npz(zb)
+    g = _gym(par)
+    g.D = zb["D"]
+    g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
+    rs = np.random.RandomState(41)
+    q0 = zb["Q"][0, 0].reshape(-1, 3)
+    lo, hi = (8, 12) if case == "pixk_dense32" else (61, 68)
+    starts = []
+    for c in range(24):
+        m = q0[rs.permutation(len(q0))[:lo + c % (hi - lo + 1)]].copy()
+        m[:, 0] = g.flux2mag_converter(np.maximum(m[:, 0], 1.5 * par["f_lim"]))
+        starts.append(m)
+    kw = dict(f_pos=True, delta=1e-6, Niter=6, Nsteps=3, dt=0.05, N_max=hi + 8,
+              P_move=[0.2, 0.4, 0.4])
+    g.run_RHMC_rj_batched(starts, list(range(500, 524)), **kw)
+    ctx = g._context()
+    P = g._params(kw["delta"], 1000, for_energy=True)
+    for l in range(kw["Niter"] + 1):
+        for c in range(len(starts)):
+            K = int(g.N_chain[l, c])
+            V, _ = ctx.energy(P, g.q_chain[l, c, :3 * K], f_pos=True)
+            assert V == g.V_chain[l, c] or (np.isnan(V) and np.isnan(g.V_chain[l, c])), (l, c, K)
+    edge = 10 if case == "pixk_dense32" else 64
+    assert (g.N_chain <= edge).any() and (g.N_chain > edge).any()
+    # a chain whose count crossed the boundary during the run
+    assert ((g.N_chain.min(0) <= edge) & (g.N_chain.max(0) > edge)).any()

@@ -155,11 +155,12 @@ def _all_paths(capi, mode, wl, n):
 
 def test_global_tables_poisoned_equal_unpoisoned(gpu_lib):
     """every table entry a launch reads, it wrote in that
-    launch.  RHMC_OPT_TABLES fills the buffer with 0xFF bytes (NaN doubles)
-    before every launch (STREAM_POISON), or takes a fresh stream-ordered pool
-    allocation per launch with (POOL_POISON) or without the fill (POOL, round
-    5's first scheme): leapfrog, energy and MH must equal the default buffer
-    bit for bit, with no chain non-finite."""
+    launch.  RHMC_TABLES_STREAM_POISON fills the buffer with 0xFF bytes (NaN
+    doubles) before every launch: leapfrog (states, iteration counts, status),
+    energy and MH must equal the default buffer bit for bit, with no chain
+    non-finite.  The pool modes (round 5's per-launch stream-ordered
+    allocation, which reproduces a defect outside the kernels) are refused by
+    the product library."""
     capi = gpu_lib
     wl = workloads.make("S256K100", n_chains=512)
     base = _all_paths(capi, capi.TABLES_STREAM, wl, wl.n_chains)
@@ -168,10 +169,16 @@ def test_global_tables_poisoned_equal_unpoisoned(gpu_lib):
     # (V is inf for a chain with a star off the image: the position support, :303-317)
     assert np.isfinite(V).mean() > 0.5 and np.isfinite(T).all() and np.isfinite(qm).all()
     assert 0.0 < acc.mean() < 1.0
-    for mode in (capi.TABLES_STREAM_POISON, capi.TABLES_POOL, capi.TABLES_POOL_POISON):
-        got = _all_paths(capi, mode, wl, wl.n_chains)
-        for a, b, name in zip(got, base, ("q", "p", "iters", "status", "V", "T", "q_mh", "acc")):
-            assert np.array_equal(a, b), (mode, name)
+    got = _all_paths(capi, capi.TABLES_STREAM_POISON, wl, wl.n_chains)
+    for a, b, name in zip(got, base, ("q", "p", "iters", "status", "V", "T", "q_mh", "acc")):
+        assert np.array_equal(a, b), name
+    ctx = capi.Context(wl.D)
+    for mode in (capi.TABLES_POOL, capi.TABLES_POOL_POISON, capi.TABLES_POOL_KEEP,
+                 capi.TABLES_POOL_SYNCFREE, capi.TABLES_POOL_BARRIER):
+        with pytest.raises(capi.RhmcError):
+            ctx.set_option(capi.OPT_TABLES, mode)
+    assert ctx.get_option(capi.OPT_TABLES) == capi.TABLES_STREAM
+    ctx.close()
 
 
 @pytest.mark.parametrize("Ks", [[65, 90, 70, 128, 88, 77, 66], [300, 257, 400]])
@@ -199,7 +206,7 @@ def test_global_tables_poisoned_ragged_and_hugek(gpu_lib, Ks):
         p[c, :3 * K] = rs.randn(3 * K) * np.sqrt(m.H(row))
     dev = torch.device("cuda:0")
     res = []
-    for mode in (capi.TABLES_STREAM, capi.TABLES_STREAM_POISON, capi.TABLES_POOL_POISON):
+    for mode in (capi.TABLES_STREAM, capi.TABLES_STREAM_POISON):
         ctx = capi.Context(D)
         ctx.set_option(capi.OPT_TABLES, mode)
         P = capi_params(capi, par)
@@ -237,3 +244,53 @@ def test_global_tables_poisoned_ragged_and_hugek(gpu_lib, Ks):
             for ca, cb in zip(r, res[0]):
                 for a, b in zip(ca, cb):
                     assert np.array_equal(a, b)
+
+
+def test_windowed_global_tables_grow_under_same_stream_threads(gpu_lib):
+    """Two host threads on ONE stream, each alternating small and large
+    launches (every large one may grow the stream's table buffer while the
+    other thread's launch holds the old one): a launch keeps a lease on the
+    buffer it was given until it is enqueued, and the old buffer is released
+    only after a sync of the stream (include/rhmc.h threading contract), so
+    each thread's chains equal a serial run."""
+    import threading
+    capi = gpu_lib
+    wl = workloads.make("S256K100", n_chains=1024)
+    P = capi.make_params(**wl.params)
+    dev = torch.device("cuda", 0)
+    q0 = torch.from_numpy(wl.q0).to(dev)
+    p0 = torch.from_numpy(wl.p0).to(dev)
+    sizes = (64, 1024, 128, 1024)
+
+    def run(ctx, q, p, stream):
+        for n in sizes:
+            ctx.leapfrog_device(P, q.data_ptr(), p.data_ptr(), n, wl.K, 1,
+                                stream=None if stream is None else stream.cuda_stream)
+    ctx = capi.Context(wl.D)
+    ref = (q0.clone(), p0.clone())
+    torch.cuda.synchronize()
+    run(ctx, ref[0], ref[1], None)
+    torch.cuda.synchronize()
+    ctx.close()
+    for rep in range(2):
+        ctx = capi.Context(wl.D)
+        s = torch.cuda.Stream(dev)
+        outs = [(q0.clone(), p0.clone()) for _ in range(2)]
+        torch.cuda.synchronize()
+        errs = []
+
+        def work(i):
+            try:
+                run(ctx, outs[i][0], outs[i][1], s)
+            except Exception as e:  # noqa: BLE001 - reported below
+                errs.append(e)
+        th = [threading.Thread(target=work, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        torch.cuda.synchronize()
+        assert not errs
+        for q, p in outs:
+            assert torch.equal(q, ref[0]) and torch.equal(p, ref[1])
+        ctx.close()
