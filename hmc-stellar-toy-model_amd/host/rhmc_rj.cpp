@@ -726,29 +726,34 @@ struct Work {
   hipStream_t s[kStreamsPerPipe] = {};
   hipEvent_t ev[4] = {};
   int64_t cap_n = 0, cap_W = 0;
-  // device
+  // device.  Buffers that cross PCIe in the same phase are adjacent, so each
+  // phase moves them in one copy: `up` = [zoff (N int64) | K (N int32, in N
+  // int64 slots) | Z (M doubles)] (the iteration's host draws), `vt` = [V (N)
+  // | T1 (N)] (V(q') and T(p', H(q')) back together); J holds a jump's q rows
+  // and p rows back to back.
   double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *Ps = nullptr, *Z = nullptr, *J = nullptr;
   double *pack = nullptr, *T0 = nullptr, *T1 = nullptr, *V = nullptr;
   int32_t* Kd = nullptr;
   int64_t *zoffd = nullptr, *idxd = nullptr;
-  // pinned host
+  void *up_d = nullptr, *vt_d = nullptr;
+  // pinned host, the same layouts
   double *Zh = nullptr, *Jh = nullptr, *recq = nullptr, *recp = nullptr;
   double *T0h = nullptr, *T1h = nullptr, *Vh = nullptr;
   int32_t* Kh = nullptr;
   int64_t *zoffh = nullptr, *idxh = nullptr;
+  void *up_h = nullptr, *vt_h = nullptr;
 
   void release() {
-    for (double* d : {Q, P, Q0, Ps, Z, J, pack, T0, T1, V}) (void)hipFree(d);
-    (void)hipFree(Kd);
-    (void)hipFree(zoffd);
+    for (double* d : {Q, P, Q0, Ps, J, pack, T0}) (void)hipFree(d);
+    for (void* d : {up_d, vt_d}) (void)hipFree(d);
     (void)hipFree(idxd);
-    for (double* h : {Zh, Jh, recq, recp, T0h, T1h, Vh}) (void)hipHostFree(h);
-    (void)hipHostFree(Kh);
-    (void)hipHostFree(zoffh);
+    for (double* h : {Jh, recq, recp, T0h}) (void)hipHostFree(h);
+    for (void* h : {up_h, vt_h}) (void)hipHostFree(h);
     (void)hipHostFree(idxh);
     Q = P = Q0 = Ps = Z = J = pack = T0 = T1 = V = nullptr;
     Kd = nullptr;
     zoffd = idxd = nullptr;
+    up_d = vt_d = up_h = vt_h = nullptr;
     Zh = Jh = recq = recp = T0h = T1h = Vh = nullptr;
     Kh = nullptr;
     zoffh = idxh = nullptr;
@@ -788,13 +793,29 @@ struct Work {
     auto hmal = [](auto** p, size_t count) {
       return hipHostMalloc((void**)p, count * sizeof(**p), hipHostMallocDefault) == hipSuccess;
     };
-    const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&Ps, M) && dmal(&Z, M) &&
-                    dmal(&J, 2 * M) && dmal(&pack, 4 * M) && dmal(&T0, N) && dmal(&T1, N) &&
-                    dmal(&V, N) && dmal(&Kd, N) && dmal(&zoffd, N) &&
-                    dmal(&idxd, kIdxRegions * N) && hmal(&Zh, M) && hmal(&Jh, 2 * M) &&
-                    hmal(&recq, M) && hmal(&recp, M) && hmal(&T0h, N) && hmal(&T1h, N) &&
-                    hmal(&Vh, N) && hmal(&Kh, N) && hmal(&zoffh, N) &&
+    double *upd = nullptr, *uph = nullptr, *vtd = nullptr, *vth = nullptr;
+    const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&Ps, M) &&
+                    dmal(&upd, 2 * N + M) && dmal(&J, 2 * M) && dmal(&pack, 4 * M) &&
+                    dmal(&T0, N) && dmal(&vtd, 2 * N) && dmal(&idxd, kIdxRegions * N) &&
+                    hmal(&uph, 2 * N + M) && hmal(&Jh, 2 * M) && hmal(&recq, M) &&
+                    hmal(&recp, M) && hmal(&T0h, N) && hmal(&vth, 2 * N) &&
                     hmal(&idxh, kIdxRegions * N);
+    up_d = upd;
+    up_h = uph;
+    vt_d = vtd;
+    vt_h = vth;
+    if (ok) {
+      zoffd = (int64_t*)upd;
+      Kd = (int32_t*)(upd + N);
+      Z = upd + 2 * N;
+      zoffh = (int64_t*)uph;
+      Kh = (int32_t*)(uph + N);
+      Zh = uph + 2 * N;
+      V = vtd;
+      T1 = vtd + N;
+      Vh = vth;
+      T1h = vth + N;
+    }
     if (!ok) {
       release();
       return fail(RHMC_ERR_NOMEM, "reversible-jump device buffers: allocation failed");
@@ -899,11 +920,14 @@ struct DevRun {
   }
   int64_t* idx_h(int region) { return w->idxh + region * w->cap_n; }
   int64_t* idx_d(int region) { return w->idxd + region * w->cap_n; }
-  // the plan's chain order as a device index list (main stream)
-  int upload_order(const Plan& pl, int region) {
+  // the plan's chain order as a device index list (main stream); tail > 0:
+  // the copy also carries the next region's first `tail` entries (staged by
+  // the caller), one H2D instead of two
+  int upload_order(const Plan& pl, int region, int64_t tail = 0) {
     std::copy(pl.order.begin(), pl.order.end(), idx_h(region));
-    if (!pl.order.empty())
-      RJ_HIP(hipMemcpyAsync(idx_d(region), idx_h(region), pl.order.size() * sizeof(int64_t),
+    const int64_t cnt = tail > 0 ? w->cap_n + tail : (int64_t)pl.order.size();
+    if (cnt > 0)
+      RJ_HIP(hipMemcpyAsync(idx_d(region), idx_h(region), (size_t)cnt * sizeof(int64_t),
                             hipMemcpyHostToDevice, w->s[0]));
     return 0;
   }
@@ -916,10 +940,10 @@ struct DevRun {
 
   // n_steps steps on chains idx (rows of Q, P)
   int trajectories(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t n_steps,
-                   int region) {
+                   int region, int64_t tail = 0) {
     if (idx.empty()) return 0;
     const Plan pl = make_plan(idx, K, ragged_ok);
-    RJ_TRY(upload_order(pl, region));
+    RJ_TRY(upload_order(pl, region, tail));
     bool aux_used = false;
     int packed = 0;
     for (const Call& c : pl.calls) {
@@ -955,9 +979,10 @@ struct DevRun {
     return 0;
   }
 
-  // V of chains idx (rows of Q) -> Vh[j] for chain order[j]; D2H on main (not synced)
+  // V of chains idx (rows of Q) -> V[j] for chain order[j]; with copy_out
+  // also D2H into Vh on main (not synced)
   int energies(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t f_pos,
-               std::vector<int64_t>& order, int region) {
+               std::vector<int64_t>& order, int region, bool copy_out = true) {
     order.clear();
     if (idx.empty()) return 0;
     const Plan pl = make_plan(idx, K, ragged_ok);
@@ -979,8 +1004,9 @@ struct DevRun {
                                       f_pos, w->s[0]))
         return engine_fail(rc, "energy");
     }
-    RJ_HIP(hipMemcpyAsync(w->Vh, w->V, pl.order.size() * sizeof(double), hipMemcpyDeviceToHost,
-                          w->s[0]));
+    if (copy_out)
+      RJ_HIP(hipMemcpyAsync(w->Vh, w->V, pl.order.size() * sizeof(double),
+                            hipMemcpyDeviceToHost, w->s[0]));
     return 0;
   }
 };
@@ -1079,9 +1105,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     const int32_t kmax = *std::max_element(Kc.begin(), Kc.end());
     const int64_t wq = std::min<int64_t>(W, 3 * (int64_t)kmax + 3);
     const int64_t wr = 3 * (int64_t)kmax;  // the record rows' live columns
-    RJ_TRY(D.upload_K());
-    RJ_HIP(hipMemcpyAsync(w->Z, w->Zh, (size_t)zt * 8, hipMemcpyHostToDevice, s0));
-    RJ_HIP(hipMemcpyAsync(w->zoffd, w->zoffh, (size_t)n * 8, hipMemcpyHostToDevice, s0));
+    std::copy(Kc.begin(), Kc.end(), w->Kh);  // [zoff | K | Z] in one H2D
+    RJ_HIP(hipMemcpyAsync(w->up_d, w->up_h, (size_t)(2 * w->cap_n + zt) * 8,
+                          hipMemcpyHostToDevice, s0));
     RJ_HIP(hipMemcpy2DAsync(w->Q, (size_t)W * 8, w->Q0, (size_t)W * 8, (size_t)wq * 8, (size_t)n,
                             hipMemcpyDeviceToDevice, s0));
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, w->Z, w->zoffd, n,
@@ -1103,8 +1129,15 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     const bool reuse = V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta;
     if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order, kIdxV0));
     RJ_HIP(hipEventRecord(w->ev[3], s0));  // T0h and Vh are on their way
+    // the jumping chains (their rows go to the host after the trajectory):
+    // their index list rides on the trajectory's order upload
+    static_assert(kIdxJump == kIdxSteps1 + 1, "adjacent index regions");
+    jump.clear();
+    for (int64_t c = 0; c < n; ++c)
+      if (R.ch[c].move != 0) jump.push_back(c);
+    std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
     // 3. the trajectory of every chain (queued behind the above)
-    RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1));
+    RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1, (int64_t)jump.size()));
     // the iteration's records while the GPU integrates
     RJ_HIP(hipStreamSynchronize(s1));
     RJ_HIP(hipEventSynchronize(w->ev[3]));
@@ -1138,26 +1171,20 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     });
     lap(1);
     // 4. the jumping chains' rows to the host, their proposals on (q, -p), back
-    jump.clear();
-    for (int64_t c = 0; c < n; ++c)
-      if (R.ch[c].move != 0) jump.push_back(c);
     const int64_t nj = (int64_t)jump.size();
     // a jumping row's columns: its 3 K stars and the one a birth / split adds
     int32_t kj = 1;
     for (int64_t c : jump) kj = std::max(kj, Kc[c]);
     const int64_t dj = std::min<int64_t>(W, 3 * (int64_t)kj + 3);
-    double* Jq = w->J;
-    double* Jp = w->J + n * W;
+    double* Jq = w->J;              // [nj][dj] q rows, then [nj][dj] p rows
+    double* Jp = w->J + nj * dj;
     int64_t* jd = D.idx_d(kIdxJump);
     if (nj > 0) {
-      std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
-      RJ_HIP(hipMemcpyAsync(jd, D.idx_h(kIdxJump), (size_t)nj * 8, hipMemcpyHostToDevice, s0));
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
       if (int rc = rhmc_rows_copy_device(ctx, w->P, W, jd, Jp, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
-      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(nj * dj) * 8, hipMemcpyDeviceToHost, s0));
-      RJ_HIP(hipMemcpyAsync(w->Jh + n * W, Jp, (size_t)(nj * dj) * 8, hipMemcpyDeviceToHost, s0));
+      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(2 * nj * dj) * 8, hipMemcpyDeviceToHost, s0));
     }
     RJ_HIP(hipStreamSynchronize(s0));
     lap(2);
@@ -1166,7 +1193,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     R.parallel(jpos, [&](int64_t j) {
       Chain& h = R.ch[jump[j]];
       double* rq = w->Jh + j * dj;
-      double* rp = w->Jh + n * W + j * dj;
+      double* rp = w->Jh + nj * dj + j * dj;
       const int64_t d = 3 * (int64_t)h.K;
       h.q.assign(rq, rq + d);
       h.p.resize((size_t)d);
@@ -1186,8 +1213,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     for (int64_t c : live) Kc[c] = R.ch[c].K;
     lap(3);
     if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
-      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(nj * dj) * 8, hipMemcpyHostToDevice, s0));
-      RJ_HIP(hipMemcpyAsync(Jp, w->Jh + n * W, (size_t)(nj * dj) * 8, hipMemcpyHostToDevice, s0));
+      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(2 * nj * dj) * 8, hipMemcpyHostToDevice, s0));
       if (int rc = rhmc_rows_copy_device(ctx, Jq, dj, nullptr, w->Q, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
       if (int rc = rhmc_rows_copy_device(ctx, Jp, dj, nullptr, w->P, W, jd, nj, (int32_t)dj, s0))
@@ -1201,11 +1227,13 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     scored.clear();
     for (int64_t c = 0; c < n; ++c)
       if (!R.ch[c].dead) scored.push_back(c);
-    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1));
+    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1, false));
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, nullptr, nullptr, n,
                                           w->T1, s0))
       return D.engine_fail(rc, "kinetic");
-    RJ_HIP(hipMemcpyAsync(w->T1h, w->T1, (size_t)n * 8, hipMemcpyDeviceToHost, s0));
+    // V(q') (order.size() values) and T1 (n) back in one copy: [V | T1]
+    RJ_HIP(hipMemcpyAsync(w->vt_h, w->vt_d, (size_t)(w->cap_n + n) * 8, hipMemcpyDeviceToHost,
+                          s0));
     RJ_HIP(hipStreamSynchronize(s0));
     for (size_t j = 0; j < order.size(); ++j) V1[order[j]] = w->Vh[j];
     lap(5);
