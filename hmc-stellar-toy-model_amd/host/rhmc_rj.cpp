@@ -1032,8 +1032,10 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
   std::vector<int64_t> all((size_t)n);
-  for (int64_t c = 0; c < n; ++c) {
-    all[c] = c;
+  for (int64_t c = 0; c < n; ++c) all[c] = c;
+  // each chain's stream (MT19937 seeding: ~2 us a chain) and the caller's
+  // rows -> Q0 (zeros past 3 K), on the pool
+  R.parallel(all, [&](int64_t c) {
     Chain& h = R.ch[c];
     if (cfg->use_states) {
       const rhmc_np_state& st = cfg->states[rec_off + c];
@@ -1043,9 +1045,6 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     }
     h.K = K[c];
     Kc[c] = K[c];
-  }
-  // the caller's rows -> Q0 (zeros past 3 K)
-  R.parallel(all, [&](int64_t c) {
     double* row = w->Zh + c * W;
     std::copy(q + c * W, q + c * W + 3 * (int64_t)K[c], row);
     std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
@@ -1289,15 +1288,15 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   // the final states
   RJ_HIP(hipMemcpyAsync(w->Zh, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s0));
   RJ_HIP(hipStreamSynchronize(s0));
-  std::copy(w->Zh, w->Zh + n * W, q);
-  for (int64_t c = 0; c < n; ++c) {
+  R.parallel(all, [&](int64_t c) {
+    std::copy(w->Zh + c * W, w->Zh + (c + 1) * W, q + c * W);
     const Chain& h = R.ch[c];
     K[c] = h.K;
     if (cfg->states) {
       rhmc_np_state& st = cfg->states[rec_off + c];
       h.rng.get_state(st.key, &st.pos, &st.has_gauss, &st.gauss);
     }
-  }
+  });
   if (phase_out)
     for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];
   return 0;

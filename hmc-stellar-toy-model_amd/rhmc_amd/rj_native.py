@@ -212,7 +212,12 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
             raise ValueError("one state per chain")
         sd = np.zeros(n, dtype=np.uint32)
     else:
-        st = np.zeros(n, dtype=STATE_DTYPE)
+        # the driver writes every chain's stream at the end; a spare buffer of
+        # the right shape (out["states"]) takes them instead of fresh memory
+        st = (out or {}).get("states")
+        if not (isinstance(st, np.ndarray) and st.dtype == STATE_DTYPE and st.shape == (n,)
+                and st.flags.c_contiguous and st.flags.writeable):
+            st = np.zeros(n, dtype=STATE_DTYPE)
         sd = np.asarray(seeds, dtype=np.int64)
         if sd.size and (sd.min() < 0 or sd.max() > 2 ** 32 - 1):
             raise ValueError("seeds must be in [0, 2**32)")
@@ -284,6 +289,5 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
         if err:
             raise err[0]
         _check(rc)
-    flat = q[np.arange(W)[None, :] < 3 * K[:, None]]     # the chains' final q, row after row
-    ends = np.cumsum(3 * K.astype(np.int64)).tolist()
-    return [flat[a:b] for a, b in zip([0] + ends[:-1], ends)], rec
+    # the chains' final q: views of each row's first 3 K entries
+    return [row[:d] for row, d in zip(q, (3 * K.astype(np.int64)).tolist())], rec

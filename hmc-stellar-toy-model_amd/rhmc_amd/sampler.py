@@ -886,11 +886,13 @@ class multi_gym(base_class):
         # inside the run.  The attributes are detached until the run succeeds,
         # so a failed run leaves None, not half-overwritten records.
         out = {}
-        for key in (("q_chain", "p_chain") if reuse_records else ()):
-            a = self.__dict__.get(key)
-            if isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3:
+        for key, attr in ((("q_chain", "q_chain"), ("p_chain", "p_chain"),
+                           ("states", "rj_rng_states")) if reuse_records else ()):
+            a = self.__dict__.get(attr)
+            if (isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3
+                    and not (key == "states" and rng_states is not None)):
                 out[key] = a
-                setattr(self, key, None)
+                setattr(self, attr, None)
             a = None
         import time
         t0 = time.perf_counter()

@@ -52,6 +52,32 @@ __global__ void thr(double* out, double seed, int iters) {
         const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0xB1, 0xF, 0xF, false);
         a0 = a0 * m + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
       }
+    } else if (MODE == 10) {  // 8 independent 32-bit integer adds (v_add_u32)
+      int i0 = __double_as_longlong(a0), i1 = i0 + 1, i2 = i0 + 2, i3 = i0 + 3, i4 = i0 + 4,
+          i5 = i0 + 5, i6 = i0 + 6, i7 = i0 + 7;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        asm volatile("v_add_u32 %0, %0, 3\n v_add_u32 %1, %1, 3\n v_add_u32 %2, %2, 3\n"
+                     " v_add_u32 %3, %3, 3\n v_add_u32 %4, %4, 3\n v_add_u32 %5, %5, 3\n"
+                     " v_add_u32 %6, %6, 3\n v_add_u32 %7, %7, 3"
+                     : "+v"(i0), "+v"(i1), "+v"(i2), "+v"(i3), "+v"(i4), "+v"(i5), "+v"(i6),
+                       "+v"(i7));
+      }
+      a0 += (double)(i0 + i1 + i2 + i3 + i4 + i5 + i6 + i7) * 1e-30;
+    } else if (MODE == 11) {  // 8 dependent 32-bit integer adds (one chain)
+      int i0 = __double_as_longlong(a0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        asm volatile("v_add_u32 %0, %0, 3\n v_add_u32 %0, %0, 3\n v_add_u32 %0, %0, 3\n"
+                     " v_add_u32 %0, %0, 3\n v_add_u32 %0, %0, 3\n v_add_u32 %0, %0, 3\n"
+                     " v_add_u32 %0, %0, 3\n v_add_u32 %0, %0, 3"
+                     : "+v"(i0));
+      a0 += (double)i0 * 1e-30;
+    } else if (MODE == 12) {  // dependent ds_bpermute chain (cross-lane through LDS)
+      int i0 = (int)__double_as_longlong(a0);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) i0 = __builtin_amdgcn_ds_bpermute(((threadIdx.x + 1) & 63) * 4, i0);
+      a0 += (double)i0 * 1e-30;
     } else if (MODE == 6) {  // exp (ocml) x8 independent
       a0 = exp(-a0); a1 = exp(-a1); a2 = exp(-a2); a3 = exp(-a3);
       a4 = exp(-a4); a5 = exp(-a5); a6 = exp(-a6); a7 = exp(-a7);
@@ -127,11 +153,12 @@ int main() {
   const double ghz = 2.4;
   const char* names[] = {"fma x8 indep", "rcp x8 indep", "fma dep chain", "fma 2 chains",
                          "mul x8 indep", "rcp:fma 1:7", "exp x8 indep", "rcp dep chain",
-                         "cvt f32->f64 x8", "dpp+fma dep x8"};
+                         "cvt f32->f64 x8", "dpp+fma dep x8", "u32 add x8 indep",
+                         "u32 add dep x8", "bpermute dep x8"};
   const int iters = 20000;
   for (int wps : {1, 2, 4}) {
     const int blocks = simds * wps;
-    float t[10];
+    float t[13];
     t[0] = run<0>(blocks, iters);
     t[1] = run<1>(blocks, iters);
     t[2] = run<2>(blocks, iters);
@@ -142,8 +169,12 @@ int main() {
     t[7] = run<7>(blocks, iters);
     t[8] = run<8>(blocks, iters);
     t[9] = run<9>(blocks, iters);
-    for (int m = 0; m < 10; ++m) {
-      const double ops = (double)wps * iters / (m == 6 ? 20 : 1) * 8;  // wave-ops per SIMD
+    t[10] = run<10>(blocks, iters);
+    t[11] = run<11>(blocks, iters);
+    t[12] = run<12>(blocks, iters);
+    for (int m = 0; m < 13; ++m) {
+      // wave-ops per SIMD (the u32 modes issue 32 adds per iteration)
+      const double ops = (double)wps * iters / (m == 6 ? 20 : 1) * (m == 10 || m == 11 ? 32 : 8);
       printf("waves/SIMD %d  %-14s %8.3f ms  %6.2f cycles/wave-op @%.1fGHz\n", wps, names[m],
              t[m], t[m] * 1e-3 * ghz * 1e9 / ops, ghz);
     }
