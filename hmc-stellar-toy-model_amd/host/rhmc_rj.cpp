@@ -26,9 +26,11 @@
 #include <condition_variable>
 #include <functional>
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <exception>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -723,8 +725,16 @@ enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions
 struct Work {
   std::mutex mu;
   int dev = -1;
+  // the pipe's host worker threads, kept between runs like the buffers
+  // (starting 16 threads per run cost ~1 ms); rebuilt when the count changes
+  std::unique_ptr<Pool> pool;
+  int pool_n = 0;
   hipStream_t s[kStreamsPerPipe] = {};
   hipEvent_t ev[4] = {};
+  // blocking-sync events: the host waits for a stream by sleeping on one of
+  // these instead of hipStreamSynchronize's spin, which took CPU from the pool
+  // threads of the other pipes (the box grants 16 CPUs to ~20 threads)
+  hipEvent_t evb[kStreamsPerPipe] = {};
   int64_t cap_n = 0, cap_W = 0;
   // device.  Buffers that cross PCIe in the same phase are adjacent, so each
   // phase moves them in one copy: `up` = [zoff (N int64) | K (N int32, in N
@@ -762,6 +772,8 @@ struct Work {
 
   // everything, streams and events included (rhmc_rj_release; `mu` held)
   void destroy() {
+    pool.reset();
+    pool_n = 0;
     if (dev < 0) return;
     (void)hipSetDevice(dev);
     for (auto& st : s)
@@ -769,6 +781,9 @@ struct Work {
     release();
     for (auto& e : ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : evb)
+      if (e) (void)hipEventDestroy(e);
+    for (auto& e : evb) e = nullptr;
     for (auto& st : s)
       if (st) (void)hipStreamDestroy(st);
     for (auto& e : ev) e = nullptr;
@@ -782,6 +797,8 @@ struct Work {
       dev = device;
       for (auto& st : s) RJ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
       for (auto& e : ev) RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      for (auto& e : evb)
+        RJ_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
     }
     if (n <= cap_n && W <= cap_W) return 0;
     for (auto& st : s) RJ_HIP(hipStreamSynchronize(st));
@@ -798,7 +815,7 @@ struct Work {
                     dmal(&upd, 2 * N + M) && dmal(&J, 2 * M) && dmal(&pack, 4 * M) &&
                     dmal(&T0, N) && dmal(&vtd, 2 * N) && dmal(&idxd, kIdxRegions * N) &&
                     hmal(&uph, 2 * N + M) && hmal(&Jh, 2 * M) && hmal(&recq, M) &&
-                    hmal(&recp, M) && hmal(&T0h, N) && hmal(&vth, 2 * N) &&
+                    hmal(&recp, M) && hmal(&T0h, 2 * N) && hmal(&vth, 2 * N) &&
                     hmal(&idxh, kIdxRegions * N);
     up_d = upd;
     up_h = uph;
@@ -931,6 +948,12 @@ struct DevRun {
                             hipMemcpyHostToDevice, w->s[0]));
     return 0;
   }
+  // the host sleeps until stream i is done (blocking-sync event)
+  int wait(int i) {
+    RJ_HIP(hipEventRecord(w->evb[i], w->s[i]));
+    RJ_HIP(hipEventSynchronize(w->evb[i]));
+    return 0;
+  }
   // aux waits for main, or main for aux
   int join(int from, int to, int e) {
     RJ_HIP(hipEventRecord(w->ev[e], w->s[from]));
@@ -979,10 +1002,10 @@ struct DevRun {
     return 0;
   }
 
-  // V of chains idx (rows of Q) -> V[j] for chain order[j]; with copy_out
-  // also D2H into Vh on main (not synced)
+  // V of chains idx (rows of Q) -> V[j] for chain order[j]; with dst_h also
+  // D2H there on main (not synced)
   int energies(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t f_pos,
-               std::vector<int64_t>& order, int region, bool copy_out = true) {
+               std::vector<int64_t>& order, int region, double* dst_h = nullptr) {
     order.clear();
     if (idx.empty()) return 0;
     const Plan pl = make_plan(idx, K, ragged_ok);
@@ -1004,8 +1027,8 @@ struct DevRun {
                                       f_pos, w->s[0]))
         return engine_fail(rc, "energy");
     }
-    if (copy_out)
-      RJ_HIP(hipMemcpyAsync(w->Vh, w->V, pl.order.size() * sizeof(double),
+    if (dst_h)
+      RJ_HIP(hipMemcpyAsync(dst_h, w->V, pl.order.size() * sizeof(double),
                             hipMemcpyDeviceToHost, w->s[0]));
     return 0;
   }
@@ -1017,6 +1040,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
                const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
                const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
                double* phase_out) {
+#ifdef RHMC_RJ_TIMING
+  const auto t_setup0 = std::chrono::steady_clock::now();
+#endif
   const int64_t W = 3 * (int64_t)cfg->N_max;
   RJ_TRY(w->ensure(dev, n, W));
   hipStream_t s0 = w->s[0], s1 = w->s[1];
@@ -1027,8 +1053,12 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.Kmax = cfg->N_max;
   R.beta.set(cfg->beta_a, cfg->beta_b);
   R.nt = nt;
-  Pool pool(nt);
-  R.pool = &pool;
+  if (!w->pool || w->pool_n != nt) {
+    w->pool.reset();
+    w->pool.reset(new Pool(nt));
+    w->pool_n = nt;
+  }
+  R.pool = w->pool.get();
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
   std::vector<int64_t> all((size_t)n);
@@ -1072,7 +1102,10 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     phase[i] += std::chrono::duration<double>(t - clk).count();
     clk = t;
   };
-  std::vector<int64_t> order, jump, live, scored, acc_rows;
+  std::vector<int64_t> order, order0, jump, live, scored, acc_rows;
+#ifdef RHMC_RJ_TIMING
+  const auto t_loop0 = std::chrono::steady_clock::now();
+#endif
   for (int64_t l = 0; l < rows_n; ++l) {
     if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
     if (cfg->n_beta > 0) R.P.beta = cfg->schedule_beta[std::min<int64_t>(l, cfg->n_beta - 1)];
@@ -1126,8 +1159,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
                                 (size_t)n, hipMemcpyDeviceToHost, s1));
     }
     const bool reuse = V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta;
-    if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order, kIdxV0));
-    RJ_HIP(hipEventRecord(w->ev[3], s0));  // T0h and Vh are on their way
+    double* V0h = w->T0h + w->cap_n;  // V(q) when not reused, read at the accept step
+    if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order0, kIdxV0, V0h));
     // the jumping chains (their rows go to the host after the trajectory):
     // their index list rides on the trajectory's order upload
     static_assert(kIdxJump == kIdxSteps1 + 1, "adjacent index regions");
@@ -1135,39 +1168,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     for (int64_t c = 0; c < n; ++c)
       if (R.ch[c].move != 0) jump.push_back(c);
     std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
-    // 3. the trajectory of every chain (queued behind the above)
+    // 3. the trajectory of every chain (queued behind the above).  The host
+    // needs T0, V(q) and the record rows only at the accept step: no wait here
     RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1, (int64_t)jump.size()));
-    // the iteration's records while the GPU integrates
-    RJ_HIP(hipStreamSynchronize(s1));
-    RJ_HIP(hipEventSynchronize(w->ev[3]));
-    if (reuse) {
-      V0 = V_end;
-    } else {
-      for (size_t j = 0; j < order.size(); ++j) V0[order[j]] = w->Vh[j];
-    }
-    R.parallel(all, [&](int64_t c) {
-      Chain& h = R.ch[c];
-      h.E0 = V0[c] + w->T0h[c];
-      const int64_t r = l * rec_stride + rec_off + c;
-      if (rec) {
-        // the rows are zero past 3 K on the device: copy the 3 K, write the zeros
-        const int64_t d = 3 * (int64_t)h.K;
-        if (rec_q) {
-          double* dst = rec->q_chain + r * W;
-          std::fill(std::copy(w->recq + c * W, w->recq + c * W + d, dst), dst + W, 0.);
-        }
-        if (rec_p) {
-          double* dst = rec->p_chain + r * W;
-          std::fill(std::copy(w->recp + c * W, w->recp + c * W + d, dst), dst + W, 0.);
-        }
-        if (rec->V_chain) rec->V_chain[r] = V0[c];
-        if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
-        if (rec->E_chain) rec->E_chain[r] = h.E0;
-        if (rec->n_stars) rec->n_stars[r] = h.K;
-        if (rec->move)
-          rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
-      }
-    });
     lap(1);
     // 4. the jumping chains' rows to the host, their proposals on (q, -p), back
     const int64_t nj = (int64_t)jump.size();
@@ -1185,7 +1188,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
         return D.engine_fail(rc, "gather");
       RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(2 * nj * dj) * 8, hipMemcpyDeviceToHost, s0));
     }
-    RJ_HIP(hipStreamSynchronize(s0));
+    RJ_TRY(D.wait(0));
     lap(2);
     std::vector<int64_t> jpos(jump.size());
     for (int64_t j = 0; j < nj; ++j) jpos[j] = j;
@@ -1226,21 +1229,47 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     scored.clear();
     for (int64_t c = 0; c < n; ++c)
       if (!R.ch[c].dead) scored.push_back(c);
-    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1, false));
+    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1));
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, nullptr, nullptr, n,
                                           w->T1, s0))
       return D.engine_fail(rc, "kinetic");
     // V(q') (order.size() values) and T1 (n) back in one copy: [V | T1]
     RJ_HIP(hipMemcpyAsync(w->vt_h, w->vt_d, (size_t)(w->cap_n + n) * 8, hipMemcpyDeviceToHost,
                           s0));
-    RJ_HIP(hipStreamSynchronize(s0));
+    RJ_TRY(D.wait(0));
+    RJ_TRY(D.wait(1));  // the record rows of the iteration's start
     for (size_t j = 0; j < order.size(); ++j) V1[order[j]] = w->Vh[j];
+    if (reuse) {
+      V0 = V_end;
+    } else {
+      for (size_t j = 0; j < order0.size(); ++j) V0[order0[j]] = V0h[j];
+    }
     lap(5);
-    // 7. accept / reject (:1072-1083, :1120-1131); accepted rows become Q0
+    // 7. the iteration's records (row l: its starting state), accept / reject
+    // (:1072-1083, :1120-1131); accepted rows become Q0
     std::vector<char> acc((size_t)n, 0);
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
       const int64_t r = l * rec_stride + rec_off + c;
+      h.E0 = V0[c] + w->T0h[c];
+      if (rec) {
+        // the rows are zero past 3 K0 on the device: copy the 3 K0, write the zeros
+        const int64_t d = 3 * (int64_t)h.K0;
+        if (rec_q) {
+          double* dst = rec->q_chain + r * W;
+          std::fill(std::copy(w->recq + c * W, w->recq + c * W + d, dst), dst + W, 0.);
+        }
+        if (rec_p) {
+          double* dst = rec->p_chain + r * W;
+          std::fill(std::copy(w->recp + c * W, w->recp + c * W + d, dst), dst + W, 0.);
+        }
+        if (rec->V_chain) rec->V_chain[r] = V0[c];
+        if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
+        if (rec->E_chain) rec->E_chain[r] = h.E0;
+        if (rec->n_stars) rec->n_stars[r] = h.K0;
+        if (rec->move)
+          rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
+      }
       bool a = false;
       if (!h.dead) {
         const double E1 = V1[c] + w->T1h[c];
@@ -1285,6 +1314,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     V_end_beta = R.P.beta;
     V_end_ok = true;
   }
+#ifdef RHMC_RJ_TIMING
+  const auto t_loop1 = std::chrono::steady_clock::now();
+#endif
   // the final states
   RJ_HIP(hipMemcpyAsync(w->Zh, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s0));
   RJ_HIP(hipStreamSynchronize(s0));
@@ -1299,6 +1331,12 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   });
   if (phase_out)
     for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];
+#ifdef RHMC_RJ_TIMING  // diagnostic build: setup / iterations / teardown of a pipe
+  const auto t_end = std::chrono::steady_clock::now();
+  auto ms = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
+  std::fprintf(stderr, "rj pipe n=%lld setup %.3f ms iterations %.3f ms teardown %.3f ms\n",
+               (long long)n, ms(t_setup0, t_loop0), ms(t_loop0, t_loop1), ms(t_loop1, t_end));
+#endif
   return 0;
 }
 

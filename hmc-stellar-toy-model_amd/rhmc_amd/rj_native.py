@@ -13,7 +13,9 @@ import numpy as np
 
 from . import capi
 
-LIB_PATH = os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so")
+# RHMC_RJ_LIB: a diagnostic build of the driver instead (tools only)
+LIB_PATH = os.environ.get("RHMC_RJ_LIB",
+                          os.path.join(os.path.dirname(capi.LIB_PATH), "librhmc_rj.so"))
 DEAD_END = 1                 # RHMC_RJ_DEAD_END
 
 EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_beta_eval",
@@ -143,12 +145,21 @@ def beta_eval(a, b, x):
     return pdf, logpdf
 
 
-def pack_starts(q_models, N_max, flux_to_count=0.):
+def _q_buf(out, n, N_max):
+    shape = (n, 3 * int(N_max))
+    if (isinstance(out, np.ndarray) and out.shape == shape and out.dtype == np.float64
+            and out.flags.c_contiguous and out.flags.writeable):
+        return out
+    return np.empty(shape)
+
+
+def pack_starts(q_models, N_max, flux_to_count=0., out=None):
     """Chain starts -> (q [n][3 N_max] zero-padded, K [n]) in one native pass.
     q_models: [K_c, 3] arrays, or one [n, K, 3] array when every chain has K
     stars — (mag, x, y) rows converted by format_q's mag2flux
     (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 — or flat
-    flux-count vectors with flux_to_count = 0."""
+    flux-count vectors with flux_to_count = 0.  out: an optional float64
+    [n][3 N_max] buffer that takes q (every row written in full)."""
     n = len(q_models)
     if n == 0:
         return np.zeros((0, 3 * int(N_max))), np.zeros(0, np.int32)
@@ -159,7 +170,7 @@ def pack_starts(q_models, N_max, flux_to_count=0.):
         if K[0] < 1 or K[0] > N_max:
             raise ValueError("every start needs 1 .. N_max stars")
         rows = np.ascontiguousarray(q_models, dtype=np.float64).reshape(-1)
-        q = np.empty((n, 3 * int(N_max)))
+        q = _q_buf(out, n, N_max)
         _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
                                         float(flux_to_count), q.ctypes.data))
         return q, K
@@ -176,7 +187,7 @@ def pack_starts(q_models, N_max, flux_to_count=0.):
     if K.min() < 1 or K.max() > N_max:
         raise ValueError("every start needs 1 .. N_max stars")
     rows = np.ascontiguousarray(rows, dtype=np.float64)
-    q = np.empty((n, 3 * int(N_max)))
+    q = _q_buf(out, n, N_max)
     _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
                                     float(flux_to_count), q.ctypes.data))
     return q, K
@@ -248,11 +259,17 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
                 and a.flags.c_contiguous and a.flags.writeable):
             return a
         return np.zeros((rows_n, n, W))
+    def rec_small(key, dtype):   # [rows_n][n] records, written in full by the driver
+        a = (out or {}).get(key)
+        if (isinstance(a, np.ndarray) and a.shape == (rows_n, n) and a.dtype == dtype
+                and a.flags.c_contiguous and a.flags.writeable):
+            return a
+        return np.zeros((rows_n, n), dtype)
     rec = {"q_chain": rec_buf("q_chain"), "p_chain": rec_buf("p_chain"),
-           "E_chain": np.zeros((rows_n, n)), "V_chain": np.zeros((rows_n, n)),
-           "T_chain": np.zeros((rows_n, n)), "accept": np.zeros((rows_n, n), np.int32),
+           "E_chain": rec_small("E_chain", np.float64), "V_chain": rec_small("V_chain", np.float64),
+           "T_chain": rec_small("T_chain", np.float64), "accept": np.zeros((rows_n, n), np.int32),
            "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),
-           "flags": np.zeros((rows_n, n), np.int32), "phase_s": np.zeros(7), "states": st}
+           "flags": rec_small("flags", np.int32), "phase_s": np.zeros(7), "states": st}
     r = RjRecord(*[rec[k].ctypes.data for k in ("q_chain", "p_chain", "E_chain", "V_chain",
                                                   "T_chain", "accept", "move", "n_stars",
                                                   "flags", "phase_s")])

@@ -864,20 +864,28 @@ class multi_gym(base_class):
         if jumps and (self.alpha is None or self.fmin is None or self.fmax is None):
             assert False                                  # :1205-1207 (prior required)
         # the starts in one native pass: [K, 3] (mag, x, y) rows through format_q's
-        # mag2flux (bit-identical to _start_q), flat q vectors (a resume) as they are
+        # mag2flux (bit-identical to _start_q), flat q vectors (a resume) as they are.
+        # With reuse_records the previous run's packed [n][3 N_max] array takes
+        # them when nothing else holds it (the returned q views keep it alive)
+        qbuf = self.__dict__.get("_rj_qbuf") if reuse_records else None
+        if not (isinstance(qbuf, np.ndarray) and sys.getrefcount(qbuf) <= 3):
+            qbuf = None
+        self._rj_qbuf = None
         if isinstance(q_models_0, np.ndarray) and q_models_0.ndim == 3:
-            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count)
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf)
             dims = None
         else:
             dims = {np.ndim(m) for m in q_models_0}
         if dims is None:
             pass
         elif dims <= {2}:
-            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count)
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf)
         elif dims <= {1}:
-            packed = rj_native.pack_starts(q_models_0, N_max)
+            packed = rj_native.pack_starts(q_models_0, N_max, out=qbuf)
         else:
-            packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max)
+            packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max,
+                                           out=qbuf)
+        qbuf = None
         P = self._params(delta, counter_max, for_energy=True)
         # reuse_records (opt-in): the previous run's q_chain / p_chain memory
         # takes this run's records when nothing but this sampler holds it (no
@@ -887,6 +895,8 @@ class multi_gym(base_class):
         # so a failed run leaves None, not half-overwritten records.
         out = {}
         for key, attr in ((("q_chain", "q_chain"), ("p_chain", "p_chain"),
+                           ("E_chain", "E_chain"), ("V_chain", "V_chain"),
+                           ("T_chain", "T_chain"), ("flags", "flag_chain"),
                            ("states", "rj_rng_states")) if reuse_records else ()):
             a = self.__dict__.get(attr)
             if (isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3
@@ -918,6 +928,8 @@ class multi_gym(base_class):
         self.N_chain = rec["n_stars"].astype(int)
         self.flag_chain = rec["flags"]
         self.rj_rng_states = rec["states"]     # every chain's stream at the end (resume)
+        if reuse_records:
+            self._rj_qbuf = packed[0]
         self.rj_phase_s = dict(zip(("draws", "V0", "steps1", "proposals", "steps2", "V1",
                                     "accept"), rec["phase_s"]))
         self.Nobjs = self.d = None

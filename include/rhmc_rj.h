@@ -142,10 +142,11 @@ typedef struct rhmc_rj_record {
                         trajectories, proposals (host), second
                         trajectories, V(q'), accept (host).  rhmc_rj_run
                         overlaps device and host work, so its phases are
-                        the host's waits: [1] momentum / T / V(q) and the
-                        record rows, [2] the first trajectories, [4] only
-                        queueing the second ones, [5] their completion
-                        with V(q') and T'                                   */
+                        the host's waits: [1] only queueing the momentum,
+                        T, V(q) and the first trajectories, [2] their
+                        completion, [4] queueing the second ones, [5]
+                        their completion with V(q') and T', [6] the
+                        iteration's record rows and the accept step        */
 } rhmc_rj_record;
 
 #define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */
