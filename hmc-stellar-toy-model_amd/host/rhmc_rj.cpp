@@ -1057,9 +1057,15 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
   std::vector<int64_t> all((size_t)n);
-  for (int64_t c = 0; c < n; ++c) all[c] = c;
+  int32_t kin = 1;
+  for (int64_t c = 0; c < n; ++c) {
+    all[c] = c;
+    kin = std::max(kin, K[c]);
+  }
   // each chain's stream (MT19937 seeding: ~2 us a chain) and the caller's
-  // rows -> Q0 (zeros past 3 K), on the pool
+  // rows' live columns (3 K_max, zeros past 3 K) -> Q0, on the pool; the
+  // rest of Q0 is zeroed on the device
+  const int64_t w0 = 3 * (int64_t)kin;
   R.parallel(all, [&](int64_t c) {
     Chain& h = R.ch[c];
     if (cfg->use_states) {
@@ -1070,11 +1076,13 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     }
     h.K = K[c];
     Kc[c] = K[c];
-    double* row = w->Zh + c * W;
+    double* row = w->Zh + c * w0;
     std::copy(q + c * W, q + c * W + 3 * (int64_t)K[c], row);
-    std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
+    std::fill(row + 3 * (int64_t)K[c], row + w0, 0.);
   });
-  RJ_HIP(hipMemcpyAsync(w->Q0, w->Zh, (size_t)(n * W) * 8, hipMemcpyHostToDevice, s0));
+  RJ_HIP(hipMemsetAsync(w->Q0, 0, (size_t)(n * W) * 8, s0));
+  RJ_HIP(hipMemcpy2DAsync(w->Q0, (size_t)W * 8, w->Zh, (size_t)w0 * 8, (size_t)w0 * 8,
+                          (size_t)n, hipMemcpyHostToDevice, s0));
   RJ_HIP(hipStreamSynchronize(s0));  // Zh is the draws' staging next
   std::vector<char> ragged_ok((size_t)cfg->N_max + 1, 0);
   {
@@ -1312,11 +1320,16 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
 #ifdef RHMC_RJ_TIMING
   const auto t_loop1 = std::chrono::steady_clock::now();
 #endif
-  // the final states
-  RJ_HIP(hipMemcpyAsync(w->Zh, w->Q0, (size_t)(n * W) * 8, hipMemcpyDeviceToHost, s0));
+  // the final states: the live columns (3 K_max) back, zeros past 3 K
+  int32_t kout = 1;
+  for (int64_t c = 0; c < n; ++c) kout = std::max(kout, R.ch[c].K);
+  const int64_t w1 = 3 * (int64_t)kout;
+  RJ_HIP(hipMemcpy2DAsync(w->Zh, (size_t)w1 * 8, w->Q0, (size_t)W * 8, (size_t)w1 * 8,
+                          (size_t)n, hipMemcpyDeviceToHost, s0));
   RJ_HIP(hipStreamSynchronize(s0));
   R.parallel(all, [&](int64_t c) {
-    std::copy(w->Zh + c * W, w->Zh + (c + 1) * W, q + c * W);
+    const int64_t d = 3 * (int64_t)R.ch[c].K;
+    std::fill(std::copy(w->Zh + c * w1, w->Zh + c * w1 + d, q + c * W), q + (c + 1) * W, 0.);
     const Chain& h = R.ch[c];
     K[c] = h.K;
     if (cfg->states) {
