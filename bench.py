@@ -339,8 +339,13 @@ def bench_rj(args, wl, gpu, world, rank):
                               g_ff=float(wl.params["g_ff"]), g_ff2=float(wl.params["g_ff2"]))
         g.num_rows, g.num_cols = wl.D.shape
         g.use_prior, g.alpha = True, 2.
-        g.fmin = mag2flux(23.3) * g.flux_to_count
+        # the workload's own magnitude range (workloads.make) and, on the
+        # big-sim geometries, the reference drivers' move parameters
+        # (RHMC-big-sim4.py:39-44: K_split 1, beta_a = beta_b = 4)
+        g.fmin = mag2flux({"B4": 20., "B3": 20.5}.get(wl.name, 23.3)) * g.flux_to_count
         g.fmax = mag2flux(15.) * g.flux_to_count
+        if wl.name in ("B4", "B3"):
+            g.K_split, g.beta_a, g.beta_b = 1., 4., 4.
         g.D = wl.D
         n_chains = wl.n_chains
         starts = []

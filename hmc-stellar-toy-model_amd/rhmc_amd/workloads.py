@@ -12,6 +12,11 @@ Beyond BASELINE's configs, the reference's own many-star drivers (dense
       stars of magnitudes 15 .. 20, :20, :30-31)
   B3  32x32, K=100, 4096 chains, 100 steps (RHMC-big-sim3.py: Nobjs = 100 of
       magnitudes 15 .. 20.5, :18, :28-29)
+  C5R C5's geometry (256x256, K=64, 8192 chains, prior) with the true stars
+      drawn over the reference drivers' magnitude range 15 .. 20
+      (RHMC-big-sim4.py:30-31), all above the flux wall: the MH line with
+      run_RHMC's f_pos=True (with C5's own stars, down to mag 23.3, the
+      posterior sits on the wall and almost every proposal has V = inf)
   S<n>K<k>  n x n, K=k, 4096 chains, 100 steps, the same parameters (kernel
             sweeps, e.g. S48K32)
 
@@ -119,11 +124,12 @@ def make(name, n_chains=None, seed_offset=0):
                            yt + 0.5 * rng.randn(nc)], 1)
         K = 1
         steps = 100 if name == "C1" else 500
-    elif name in ("C3", "C5", "B3", "B4") or re.fullmatch(r"S\d+K\d+", name):
+    elif name in ("C3", "C5", "C5R", "B3", "B4") or re.fullmatch(r"S\d+K\d+", name):
         if name[0] == "S":
             n, K = (int(v) for v in re.fullmatch(r"S(\d+)K(\d+)", name).groups())
         else:
-            n, K = {"C3": (48, 10), "C5": (256, 64), "B3": (32, 100), "B4": (32, 51)}[name]
+            n, K = {"C3": (48, 10), "C5": (256, 64), "C5R": (256, 64), "B3": (32, 100),
+                    "B4": (32, 51)}[name]
         par, ftc = base_params(dt=0.05, g_xx=0.05, g_ff=4., g_ff2=4.,
                                use_prior=(name != "C3"), alpha=2.)
         if par["use_prior"]:
@@ -134,11 +140,11 @@ def make(name, n_chains=None, seed_offset=0):
                 (1 - a) / (fmax ** (1 - a) - fmin ** (1 - a)))
         # true magnitudes: down to 23.3 for BASELINE's C3 / C5 (below the flux
         # wall at 23); the reference drivers' ranges for B4 / B3
-        mag_hi = {"B4": 20., "B3": 20.5}.get(name, 23.3)
+        mag_hi = {"B4": 20., "B3": 20.5, "C5R": 20.}.get(name, 23.3)
         ft, xt, yt = _powlaw_stars(img_rng, K, n, ftc, mag_hi=mag_hi)
         D = _image(n, [(22.5 - 2.5 * np.log10(a / ftc), b, c) for a, b, c in zip(ft, xt, yt)],
                    ftc, par["B_count"], par["fwhm_pix"], img_rng)
-        nc = ({"C3": 16384, "C5": 8192}.get(name, 4096)) if n_chains is None else n_chains
+        nc = ({"C3": 16384, "C5": 8192, "C5R": 8192}.get(name, 4096)) if n_chains is None else n_chains
         # chains start at the truth, perturbed (flux x lognormal 10%, 0.5 px)
         q0 = np.empty((nc, 3 * K))
         q0[:, 0::3] = ft * np.exp(0.1 * rng.randn(nc, K))

@@ -35,11 +35,13 @@ declare -A LINE=(
   [c2_mh_10x50]="--mode mh --mh-iter 10 --leap 50 --no-cpu --steps 4 --warmup 1"
   [c3_mh_5x50]="--workload C3 --mode mh --mh-iter 5 --leap 50 --no-cpu --steps 4 --warmup 1"
   [c5_mh_5x10]="--workload C5 --mode mh --mh-iter 5 --leap 10 --no-cpu --steps 2 --warmup 1 --f-pos 1"
+  [c5r_mh_5x10]="--workload C5R --mode mh --mh-iter 5 --leap 10 --no-cpu --steps 2 --warmup 1 --f-pos 1"
+  [c5r_mh_5x50]="--workload C5R --mode mh --mh-iter 5 --leap 50 --no-cpu --steps 2 --warmup 1 --f-pos 1"
   [rj_b4]="--workload B4 --mode rj --steps 5 --warmup 1 --no-cpu"
   [rj_bigsim4]="--workload BIGSIM4 --mode rj --steps 5 --warmup 1 --no-cpu"
   [rj_b4_16k]="--workload B4 --mode rj --chains 16384 --steps 3 --warmup 1 --no-cpu"
 )
-ORDER="c2 c1 c3 c4 c4_shard c5 c5_shard b4 b3 c2_mh_10x50 c3_mh_5x50 c5_mh_5x10 rj_b4 rj_bigsim4 rj_b4_16k"
+ORDER="c2 c1 c3 c4 c4_shard c5 c5_shard b4 b3 c2_mh_10x50 c3_mh_5x50 c5_mh_5x10 c5r_mh_5x10 c5r_mh_5x50 rj_b4 rj_bigsim4 rj_b4_16k"
 
 line() {  # name: one bench line into $O/<name>.json, summary printed
   local n=$1
