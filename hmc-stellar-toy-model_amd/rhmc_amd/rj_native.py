@@ -8,6 +8,7 @@ librhmc_rj.so raises (build: __graft_entry__.build() or
 """
 import ctypes
 import os
+from collections.abc import Sequence
 
 import numpy as np
 
@@ -115,6 +116,23 @@ def lib():
 def _check(rc):
     if rc != capi.RHMC_OK:
         raise capi.RhmcError(rc, _lib.rhmc_rj_last_error().decode(errors="replace"))
+
+
+class RowViews(Sequence):
+    """The chains' final q as a read-on-demand sequence: item c is a view of
+    row c's first 3 K[c] entries (building 4,096 views up front cost ~1.4 ms
+    a run)."""
+
+    def __init__(self, q, K):
+        self._q, self._d = q, 3 * np.asarray(K, dtype=np.int64)
+
+    def __len__(self):
+        return len(self._d)
+
+    def __getitem__(self, c):
+        if isinstance(c, slice):
+            return [self[i] for i in range(*c.indices(len(self)))]
+        return self._q[c, :self._d[c]]
 
 
 def release(device=-1):
@@ -306,5 +324,5 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
         if err:
             raise err[0]
         _check(rc)
-    # the chains' final q: views of each row's first 3 K entries
-    return [row[:d] for row, d in zip(q, (3 * K.astype(np.int64)).tolist())], rec
+    # the chains' final q: views of each row's first 3 K entries, on demand
+    return RowViews(q, K), rec
