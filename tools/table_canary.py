@@ -29,7 +29,7 @@ for mode in [int(m) for m in sys.argv[1:]]:
     q = torch.from_numpy(wl.q0).to(dev)
     acc = torch.zeros((5, wl.n_chains), dtype=torch.int32, device=dev)
     torch.cuda.synchronize()
-    out = (ctypes.c_int64 * 3)()
+    out = (ctypes.c_int64 * 5)()
     fn(out)   # reset
     rates = []
     for launch in range(3):
@@ -40,6 +40,7 @@ for mode in [int(m) for m in sys.argv[1:]]:
         rates.append(float(acc.float().mean()))
     fn(out)
     ctx.close()
-    print("tables=%d accept=%s conflicts total=%d gradient=%d potential=%d q_sum=%.17g"
-          % (mode, ["%.6f" % r for r in rates], out[0], out[1], out[2],
+    print("tables=%d accept=%s conflicts total=%d gradient=%d potential=%d bumps by "
+          "gradients=%d potentials=%d q_sum=%.17g"
+          % (mode, ["%.6f" % r for r in rates], out[0], out[1], out[2], out[3], out[4],
              float(q.double().sum())), flush=True)
