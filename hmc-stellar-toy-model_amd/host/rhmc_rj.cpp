@@ -36,6 +36,7 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
 #include <hip/hip_runtime_api.h>
 
 #include "np_legacy.hpp"
@@ -52,6 +53,52 @@ int fail(int code, const std::string& msg) {
 }
 
 constexpr double kPi = 3.141592653589793;  // np.pi
+
+// ------------------------------------------------------------ record rows
+// One [3 N_max] row of a record or of the final states: src[0, d) then zeros
+// to `zero_to` (W, or less where the caller's row is known to be zero past it:
+// rhmc_rj_config::records_zero_padded).  A full row goes out with
+// non-temporal stores: the q_chain / p_chain records are 2 x 3 N_max doubles
+// per chain and iteration (24 MB per iteration at 4,096 chains and N_max 120,
+// most of it the zero padding), written once and not read back by the run;
+// plain stores first pull every destination line into the cache, which
+// halved the host's record bandwidth (tools/rec_write_bench.cpp).  The
+// caller issues _mm_sfence() before the rows are handed on.
+void put_row(double* dst, const double* src, int64_t d, int64_t zero_to, int64_t W) {
+  if (zero_to < W) {
+    std::fill(std::copy(src, src + d, dst), dst + zero_to, 0.);
+    return;
+  }
+  int64_t i = 0;
+  if (reinterpret_cast<uintptr_t>(dst) & 15) {  // to a 16-byte boundary
+    dst[0] = d > 0 ? src[0] : 0.;
+    i = 1;
+  }
+  for (; i + 2 <= d; i += 2) _mm_stream_pd(dst + i, _mm_loadu_pd(src + i));
+  if (i < d) {  // one live value left
+    if (i + 2 <= W) {
+      _mm_stream_pd(dst + i, _mm_set_pd(0., src[i]));
+      i += 2;
+    } else {
+      dst[i] = src[i];
+      ++i;
+    }
+  }
+  const __m128d z = _mm_setzero_pd();
+  for (; i + 2 <= W; i += 2) _mm_stream_pd(dst + i, z);
+  if (i < W) dst[i] = 0.;
+}
+
+// The zero fill's end for record row r: with records_zero_padded the row
+// holds zeros past 3 n_stars[r] (the previous run's count), so the fill stops
+// at the larger of that and the new width d; else the whole row
+int64_t zero_end(const rhmc_rj_config* cfg, const rhmc_rj_record* rec, int64_t r, int64_t d,
+                 int64_t W) {
+  if (!cfg->records_zero_padded) return W;
+  const int32_t old = rec->n_stars[r];
+  if (old < 1 || old > cfg->N_max) return W;
+  return std::max(d, 3 * (int64_t)old);
+}
 
 // ------------------------------------------------------------ model helpers
 // H(q) of one star (sampler.py _H_vec, sampler_RHMC.py:260-292): Hd = (H_ff,
@@ -452,7 +499,8 @@ struct Run {
 int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, const int32_t* K,
           const uint32_t* seeds, int64_t n) {
   if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
-  if (cfg->reserved != 0) return fail(RHMC_ERR_ARG, "config.reserved must be 0");
+  if (cfg->records_zero_padded != 0 && cfg->records_zero_padded != 1)
+    return fail(RHMC_ERR_ARG, "records_zero_padded must be 0 or 1");
   if (cfg->n_pipes < 0 || cfg->n_pipes > kMaxPipes)
     return fail(RHMC_ERR_ARG, "n_pipes must be in [0, 8]");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
@@ -484,6 +532,12 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
     return fail(RHMC_ERR_ARG, "jumps need fmin, fmax, K_split, beta_a, beta_b > 0");
   for (int64_t c = 0; c < n; ++c)
     if (K[c] < 1 || K[c] > cfg->N_max) return fail(RHMC_ERR_ARG, "K[c] must be in [1, N_max]");
+  return 0;
+}
+
+int check_records(const rhmc_rj_config* cfg, const rhmc_rj_record* rec) {
+  if (cfg->records_zero_padded && !(rec && rec->n_stars))
+    return fail(RHMC_ERR_ARG, "records_zero_padded needs the n_stars record");
   return 0;
 }
 
@@ -583,14 +637,11 @@ int run(const rhmc_rj_physics* phys, const rhmc_params* P0,
       h.E0 = V0[c] + T0[c];
       const int64_t r = l * rec_stride + rec_off + c;
       if (rec) {
-        if (rec->q_chain) {  // the state, zero-padded to 3 N_max
-          double* row = rec->q_chain + r * W;
-          std::fill(std::copy(h.q.begin(), h.q.end(), row), row + W, 0.);
-        }
-        if (rec->p_chain) {
-          double* row = rec->p_chain + r * W;
-          std::fill(std::copy(h.p.begin(), h.p.end(), row), row + W, 0.);
-        }
+        // the state, zero-padded to 3 N_max (read n_stars[r] before it is rewritten)
+        const int64_t d = 3 * (int64_t)h.K, zt = zero_end(cfg, rec, r, d, W);
+        if (rec->q_chain) put_row(rec->q_chain + r * W, h.q.data(), d, zt, W);
+        if (rec->p_chain) put_row(rec->p_chain + r * W, h.p.data(), d, zt, W);
+        _mm_sfence();
         if (rec->V_chain) rec->V_chain[r] = V0[c];
         if (rec->T_chain) rec->T_chain[r] = T0[c];
         if (rec->E_chain) rec->E_chain[r] = h.E0;
@@ -670,8 +721,8 @@ int run(const rhmc_rj_physics* phys, const rhmc_params* P0,
     for (int i = 0; i < 7; ++i) phase_out[i] += phase[i];
   for (int64_t c = 0; c < n; ++c) {
     const Chain& h = R.ch[c];
-    std::fill(q + c * W, q + (c + 1) * W, 0.);
-    std::copy(h.q.begin(), h.q.end(), q + c * W);
+    put_row(q + c * W, h.q.data(), 3 * (int64_t)h.K, W, W);
+    _mm_sfence();
     K[c] = h.K;
     if (cfg->states) {
       rhmc_np_state& st = cfg->states[rec_off + c];
@@ -1256,16 +1307,12 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       const int64_t r = l * rec_stride + rec_off + c;
       h.E0 = V0[c] + w->T0h[c];
       if (rec) {
-        // the rows are zero past 3 K0 on the device: copy the 3 K0, write the zeros
-        const int64_t d = 3 * (int64_t)h.K0;
-        if (rec_q) {
-          double* dst = rec->q_chain + r * W;
-          std::fill(std::copy(w->recq + c * W, w->recq + c * W + d, dst), dst + W, 0.);
-        }
-        if (rec_p) {
-          double* dst = rec->p_chain + r * W;
-          std::fill(std::copy(w->recp + c * W, w->recp + c * W + d, dst), dst + W, 0.);
-        }
+        // the rows are zero past 3 K0 on the device: copy the 3 K0, write the
+        // zeros (read n_stars[r] before it is rewritten)
+        const int64_t d = 3 * (int64_t)h.K0, zt = zero_end(cfg, rec, r, d, W);
+        if (rec_q) put_row(rec->q_chain + r * W, w->recq + c * W, d, zt, W);
+        if (rec_p) put_row(rec->p_chain + r * W, w->recp + c * W, d, zt, W);
+        _mm_sfence();
         if (rec->V_chain) rec->V_chain[r] = V0[c];
         if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
         if (rec->E_chain) rec->E_chain[r] = h.E0;
@@ -1328,8 +1375,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
                           (size_t)n, hipMemcpyDeviceToHost, s0));
   RJ_HIP(hipStreamSynchronize(s0));
   R.parallel(all, [&](int64_t c) {
-    const int64_t d = 3 * (int64_t)R.ch[c].K;
-    std::fill(std::copy(w->Zh + c * w1, w->Zh + c * w1 + d, q + c * W), q + (c + 1) * W, 0.);
+    put_row(q + c * W, w->Zh + c * w1, 3 * (int64_t)R.ch[c].K, W, W);
+    _mm_sfence();
     const Chain& h = R.ch[c];
     K[c] = h.K;
     if (cfg->states) {
@@ -1432,6 +1479,7 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
                         int64_t n, const rhmc_rj_record* rec) {
   try {
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
+    if (int rc = check_records(cfg, rec)) return rc;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};
     const int nt = host_threads(cfg);
     // with pipes > 1 the callbacks are called from that many threads at once
@@ -1453,6 +1501,7 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
   try {
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
+    if (int rc = check_records(cfg, rec)) return rc;
     const double* dimg = nullptr;
     if (int rc = rhmc_ctx_image_device(ctx, &dimg)) return rc;
     if (!dimg) return fail(RHMC_ERR_ARG, "context has no image");

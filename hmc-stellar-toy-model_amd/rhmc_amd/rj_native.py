@@ -41,7 +41,7 @@ class RjConfig(ctypes.Structure):
                 ("rows", ctypes.c_int32), ("cols", ctypes.c_int32),
                 ("n_threads", ctypes.c_int32), ("n_g_ff2", ctypes.c_int32),
                 ("n_beta", ctypes.c_int32), ("n_pipes", ctypes.c_int32),
-                ("use_states", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("use_states", ctypes.c_int32), ("records_zero_padded", ctypes.c_int32),
                 ("P_move", ctypes.c_double * 3), ("fmin", ctypes.c_double),
                 ("fmax", ctypes.c_double), ("K_split", ctypes.c_double),
                 ("beta_a", ctypes.c_double), ("beta_b", ctypes.c_double),
@@ -213,7 +213,7 @@ def pack_starts(q_models, N_max, flux_to_count=0., out=None):
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0, n_pipes=0, states=None, packed=None, out=None):
+        n_threads=0, n_pipes=0, states=None, packed=None, out=None, zero_padded=False):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
     vectors, or None with packed = (q [n][3 N_max], K [n]) from pack_starts.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
@@ -221,7 +221,10 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     or an array of STATE_DTYPE rows to start from (then seeds may be None).
     out: optional {"q_chain": a, "p_chain": b} float64 [n_iter+1][n][3 N_max]
     buffers the records are written into (overwritten in full; others are
-    allocated).  Returns (q list, record dict); record["states"] holds every chain's stream
+    allocated; "n_stars" [n_iter+1][n] int32 likewise).  zero_padded: the
+    out q_chain / p_chain rows are zero past 3 out["n_stars"][row] (the
+    previous run's records: rhmc_rj_config::records_zero_padded), so only
+    the columns a row can have used are rewritten.  Returns (q list, record dict); record["states"] holds every chain's stream
     at the end (pass it back as `states` to resume)."""
     W = 3 * int(N_max)
     if packed is not None:
@@ -263,7 +266,8 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     sb, nb = arr(schedule_beta)
     pm = (ctypes.c_double * 3)(*[float(v) for v in P_move])
     cfg = RjConfig(int(n_iter), int(n_steps), int(N_max), int(f_pos), int(rows), int(cols),
-                   int(n_threads), ng, nb, int(n_pipes), int(states is not None), 0, pm,
+                   int(n_threads), ng, nb, int(n_pipes), int(states is not None),
+                   int(bool(zero_padded)), pm,
                    float(fmin), float(fmax), float(K_split), float(beta_a), float(beta_b), sg,
                    sb, st.ctypes.data if n else None)
     rows_n = int(n_iter) + 1
@@ -286,7 +290,7 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     rec = {"q_chain": rec_buf("q_chain"), "p_chain": rec_buf("p_chain"),
            "E_chain": rec_small("E_chain", np.float64), "V_chain": rec_small("V_chain", np.float64),
            "T_chain": rec_small("T_chain", np.float64), "accept": np.zeros((rows_n, n), np.int32),
-           "move": np.zeros((rows_n, n), np.int32), "n_stars": np.zeros((rows_n, n), np.int32),
+           "move": np.zeros((rows_n, n), np.int32), "n_stars": rec_small("n_stars", np.int32),
            "flags": rec_small("flags", np.int32), "phase_s": np.zeros(7), "states": st}
     r = RjRecord(*[rec[k].ctypes.data for k in ("q_chain", "p_chain", "E_chain", "V_chain",
                                                   "T_chain", "accept", "move", "n_stars",

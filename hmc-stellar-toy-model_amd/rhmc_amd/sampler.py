@@ -893,17 +893,26 @@ class multi_gym(base_class):
         # argument) — fresh arrays of this size cost a page fault per 4 KiB
         # inside the run.  The attributes are detached until the run succeeds,
         # so a failed run leaves None, not half-overwritten records.
-        out = {}
+        # The q_chain / p_chain records such a run returns are read-only and
+        # zero past 3 N_chain in every row, and their int32 star counts stay
+        # with them (_rj_nstars): the next run writes only the columns a row
+        # can have used (records_zero_padded) instead of all 3 N_max
+        out, padded = {}, True
         for key, attr in ((("q_chain", "q_chain"), ("p_chain", "p_chain"),
                            ("E_chain", "E_chain"), ("V_chain", "V_chain"),
                            ("T_chain", "T_chain"), ("flags", "flag_chain"),
+                           ("n_stars", "_rj_nstars"),
                            ("states", "rj_rng_states")) if reuse_records else ()):
             a = self.__dict__.get(attr)
             if (isinstance(a, np.ndarray) and a.base is None and sys.getrefcount(a) <= 3
                     and not (key == "states" and rng_states is not None)):
+                if key in ("q_chain", "p_chain") and a.flags.writeable:
+                    padded = False   # not this path's read-only records: no claim on them
+                a.flags.writeable = True
                 out[key] = a
                 setattr(self, attr, None)
             a = None
+        self._rj_nstars = None
         import time
         t0 = time.perf_counter()
         q_end, rec = rj_native.run(
@@ -914,7 +923,7 @@ class multi_gym(base_class):
             n_pipes=n_pipes, states=(None if rng_states is None else
                                      rng_states if isinstance(rng_states, np.ndarray)
                                      else rj_native.states_from(rng_states)), packed=packed,
-            out=out)
+            out=out, zero_padded=padded and "n_stars" in out)
         out = None
         self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
@@ -930,6 +939,9 @@ class multi_gym(base_class):
         self.rj_rng_states = rec["states"]     # every chain's stream at the end (resume)
         if reuse_records:
             self._rj_qbuf = packed[0]
+            self._rj_nstars = rec["n_stars"]
+            self.q_chain.flags.writeable = False
+            self.p_chain.flags.writeable = False
         self.rj_phase_s = dict(zip(("draws", "V0", "steps1", "proposals", "steps2", "V1",
                                     "accept"), rec["phase_s"]))
         self.Nobjs = self.d = None

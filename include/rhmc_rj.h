@@ -111,7 +111,12 @@ typedef struct rhmc_rj_config {
   int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
                             seeds[c] (a checkpoint of an earlier run, or any
                             RandomState's get_state(): continue its stream)        */
-  int32_t reserved;      /* must be 0                                                */
+  int32_t records_zero_padded; /* 0, or 1: the caller's q_chain / p_chain rows are
+                            zero past 3 n_stars[r] on entry, n_stars holding the
+                            counts of the rows they hold (a previous run's records
+                            of this shape, or zeros: any width is zero-padded past
+                            3); the driver then writes a row's zeros only up to its
+                            old width.  Needs rec->n_stars.  Was `reserved` (0)  */
   double P_move[3];      /* within / birth-death / split-merge probabilities         */
   double fmin, fmax;     /* power-law flux prior range, counts (:1221)               */
   double K_split;        /* split offset scale (:1300)                               */

@@ -229,6 +229,18 @@ def test_native_record_buffers_reused_only_when_unreferenced(gpu_lib):
     before = view.copy()
     g.run_RHMC_rj_batched(starts, list(range(100, 124)), **kw)
     np.testing.assert_array_equal(view, before)
+    # reused records come back read-only and are rewritten only up to each
+    # row's old width (records_zero_padded); records a caller made writable
+    # and wrote into are rewritten whole
+    assert not g.q_chain.flags.writeable and not g.p_chain.flags.writeable
+    view = before = None
+    g.run_RHMC_rj_batched(starts, list(range(24)), **kw)
+    np.testing.assert_array_equal(g.q_chain, first)
+    g.q_chain.flags.writeable = True
+    g.q_chain[...] = 5.
+    g.run_RHMC_rj_batched(starts, list(range(100, 124)), **kw)
+    np.testing.assert_array_equal(g.q_chain, fresh.q_chain)
+    np.testing.assert_array_equal(g.p_chain, fresh.p_chain)
 
 
 def test_native_recorded_V_dense_ragged(gpu_lib):

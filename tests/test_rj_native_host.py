@@ -79,7 +79,7 @@ def test_scipy_beta_rvs_is_the_replica(rj):
     assert a == r.beta(2., 2.)
 
 
-def _native(rj, g, starts, seeds, kw, n_threads=4, n_pipes=1):
+def _native(rj, g, starts, seeds, kw, n_threads=4, n_pipes=1, **extra):
     from rhmc_amd import capi
     qms = [g.format_q(m.copy()) for m in starts]
     P = g._params(for_energy=True)
@@ -92,7 +92,7 @@ def _native(rj, g, starts, seeds, kw, n_threads=4, n_pipes=1):
     return rj.run(P, qms, seeds, kw["Niter"], kw["Nsteps"], kw["N_max"], kw["P_move"],
                   capi.V_FLUX_WALL if kw["f_pos"] else 0, g.num_rows, g.num_cols, g.fmin, g.fmax,
                   g.K_split, g.beta_a, g.beta_b, physics=(lambda q, fp: fake_V(q), steps),
-                  n_threads=n_threads, n_pipes=n_pipes)
+                  n_threads=n_threads, n_pipes=n_pipes, **extra)
 
 
 def _clean(g, N_max):
@@ -164,6 +164,38 @@ def test_dead_ends_are_rejected_and_threads_do_not_matter(rj):
     assert r1["n_stars"][l + 1, c] == r1["n_stars"][l, c]
     assert np.array_equal(r1["q_chain"][l + 1, c], r1["q_chain"][l, c])
     assert all(q.size % 3 == 0 and 3 <= q.size <= 18 for q in q4)
+
+
+@pytest.mark.parametrize("n_pipes", [1, 3])
+def test_zero_padded_records_equal_fresh_records(rj, n_pipes):
+    """records_zero_padded (include/rhmc_rj.h): a second run written into the
+    first run's q_chain / p_chain, told that their rows are zero past 3
+    n_stars[row], rewrites only the columns a row can have used — and its
+    records equal a fresh run's bit for bit, padding included (rows whose
+    star count shrank between the runs get their old columns zeroed).  A
+    star-count record of zeros (no claim) makes the driver write whole rows."""
+    starts = STARTS * 6
+    kw = dict(f_pos=True, Niter=15, Nsteps=2, dt=0.05, N_max=10, P_move=[0.2, 0.4, 0.4])
+    _, a = _native(rj, _gym(), starts, list(range(300, 324)), kw, n_pipes=n_pipes)
+    seeds_b = list(range(500, 524))
+    _, fresh = _native(rj, _gym(), starts, seeds_b, kw, n_pipes=n_pipes)
+    assert (a["n_stars"] != fresh["n_stars"]).any()
+    assert (a["n_stars"] > fresh["n_stars"]).any()      # some rows shrink between the runs
+    out = {k: a[k] for k in ("q_chain", "p_chain", "n_stars")}
+    _, b = _native(rj, _gym(), starts, seeds_b, kw, n_pipes=n_pipes, out=out, zero_padded=True)
+    assert b["q_chain"] is a["q_chain"] and b["n_stars"] is a["n_stars"]
+    for k in fresh:
+        if k not in ("phase_s", "states"):
+            assert np.array_equal(b[k], fresh[k]), k
+    # no claim: garbage past every row's columns, star counts zero -> whole rows
+    q = np.full_like(fresh["q_chain"], 7.)
+    p = np.full_like(fresh["p_chain"], -7.)
+    out = {"q_chain": q, "p_chain": p, "n_stars": np.zeros_like(fresh["n_stars"])}
+    _, c = _native(rj, _gym(), starts, seeds_b, kw, n_pipes=n_pipes, out=out, zero_padded=True)
+    assert np.array_equal(c["q_chain"], fresh["q_chain"])
+    assert np.array_equal(c["p_chain"], fresh["p_chain"])
+    # (a claim without the star-count record and a flag of 2 are refused:
+    # tests/native/rj_asan.cpp)
 
 
 def test_argument_errors(rj):
