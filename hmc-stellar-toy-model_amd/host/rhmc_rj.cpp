@@ -787,32 +787,38 @@ struct Work {
   // device.  Buffers that cross PCIe in the same phase are adjacent, so each
   // phase moves them in one copy: `up` = [zoff (N int64) | K (N int32, in N
   // int64 slots) | Z (M doubles)] (the iteration's host draws), `vt` = [V (N)
-  // | T1 (N)] (V(q') and T(p', H(q')) back together); J holds a jump's q rows
-  // and p rows back to back.
-  double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *Ps = nullptr, *Z = nullptr, *J = nullptr;
+  // | T1 (N)] (V(q') and T(p', H(q')) back together); the jumps' q rows and
+  // p rows sit back to back in Jh (pinned, mapped) below.
+  double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *Ps = nullptr, *Z = nullptr;
   double *pack = nullptr, *T0 = nullptr, *T1 = nullptr, *V = nullptr;
   int32_t* Kd = nullptr;
   int64_t *zoffd = nullptr, *idxd = nullptr;
   void *up_d = nullptr, *vt_d = nullptr;
   // pinned host, the same layouts
   double *Zh = nullptr, *Jh = nullptr, *recq = nullptr, *recp = nullptr;
+  // Jh's device address: the jump rows cross PCIe without the copy engines —
+  // the gather kernel writes them into Jh and the scatter kernel reads them
+  // back from it (coherent pinned memory, mapped into the device's space).
+  // An SDMA H2D copy of those rows stalled the host 7-8 ms at a pipe's first
+  // iterations (profiles/r06_rj/, RHMC_RJ_TIMING build)
+  double* Jh_d = nullptr;
   double *T0h = nullptr, *T1h = nullptr, *Vh = nullptr;
   int32_t* Kh = nullptr;
   int64_t *zoffh = nullptr, *idxh = nullptr;
   void *up_h = nullptr, *vt_h = nullptr;
 
   void release() {
-    for (double* d : {Q, P, Q0, Ps, J, pack, T0}) (void)hipFree(d);
+    for (double* d : {Q, P, Q0, Ps, pack, T0}) (void)hipFree(d);
     for (void* d : {up_d, vt_d}) (void)hipFree(d);
     (void)hipFree(idxd);
     for (double* h : {Jh, recq, recp, T0h}) (void)hipHostFree(h);
     for (void* h : {up_h, vt_h}) (void)hipHostFree(h);
     (void)hipHostFree(idxh);
-    Q = P = Q0 = Ps = Z = J = pack = T0 = T1 = V = nullptr;
+    Q = P = Q0 = Ps = Z = pack = T0 = T1 = V = nullptr;
     Kd = nullptr;
     zoffd = idxd = nullptr;
     up_d = vt_d = up_h = vt_h = nullptr;
-    Zh = Jh = recq = recp = T0h = T1h = Vh = nullptr;
+    Zh = Jh = recq = recp = T0h = T1h = Vh = Jh_d = nullptr;
     Kh = nullptr;
     zoffh = idxh = nullptr;
     cap_n = cap_W = 0;
@@ -855,11 +861,16 @@ struct Work {
     auto hmal = [](auto** p, size_t count) {
       return hipHostMalloc((void**)p, count * sizeof(**p), hipHostMallocDefault) == hipSuccess;
     };
+    auto hmap = [](auto** p, size_t count) {  // coherent, mapped: kernels read / write it
+      return hipHostMalloc((void**)p, count * sizeof(**p),
+                           hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+    };
     double *upd = nullptr, *uph = nullptr, *vtd = nullptr, *vth = nullptr;
     const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&Ps, M) &&
-                    dmal(&upd, 2 * N + M) && dmal(&J, 2 * M) && dmal(&pack, 4 * M) &&
+                    dmal(&upd, 2 * N + M) && dmal(&pack, 4 * M) &&
                     dmal(&T0, N) && dmal(&vtd, 2 * N) && dmal(&idxd, kIdxRegions * N) &&
-                    hmal(&uph, 2 * N + M) && hmal(&Jh, 2 * M) && hmal(&recq, M) &&
+                    hmal(&uph, 2 * N + M) && hmap(&Jh, 2 * M) &&
+                    hipHostGetDevicePointer((void**)&Jh_d, Jh, 0) == hipSuccess && hmal(&recq, M) &&
                     hmal(&recp, M) && hmal(&T0h, 2 * N) && hmal(&vth, 2 * N) &&
                     hmal(&idxh, kIdxRegions * N);
     up_d = upd;
@@ -1018,9 +1029,19 @@ struct DevRun {
     for (const Call& c : pl.calls) {
       const int64_t* rows = idx_d(region) + c.off;
       if (c.ragged) {
+#ifdef RHMC_RJ_TIMING  // diagnostic build: a launch call that blocks
+        const auto tl0 = std::chrono::steady_clock::now();
+#endif
         if (int rc = rhmc_leapfrog_ragged_device(ctx, P, w->Q, w->P, W, rows, w->Kd, c.n, c.Kmin,
                                                  c.Kmax, n_steps, w->s[0]))
           return engine_fail(rc, "ragged steps");
+#ifdef RHMC_RJ_TIMING
+        const double tl = std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0)
+                              .count() * 1e3;
+        if (tl > 0.2)
+          std::fprintf(stderr, "rj slow launch: steps K %d-%d n %lld %.3f ms\n", c.Kmin, c.Kmax,
+                       (long long)c.n, tl);
+#endif
         continue;
       }
       // packed: gather, fixed-K steps, scatter — alternate groups onto aux
@@ -1060,9 +1081,19 @@ struct DevRun {
     for (const Call& c : pl.calls) {
       const int64_t* rows = idx_d(region) + c.off;
       if (c.ragged) {
+#ifdef RHMC_RJ_TIMING
+        const auto tl0 = std::chrono::steady_clock::now();
+#endif
         if (int rc = rhmc_energy_ragged_device(ctx, P, w->Q, W, rows, w->Kd, c.n, c.Kmin, c.Kmax,
                                                f_pos, w->V + c.off, w->s[0]))
           return engine_fail(rc, "ragged energy");
+#ifdef RHMC_RJ_TIMING
+        const double tl = std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0)
+                              .count() * 1e3;
+        if (tl > 0.2)
+          std::fprintf(stderr, "rj slow launch: energy K %d-%d n %lld %.3f ms\n", c.Kmin, c.Kmax,
+                       (long long)c.n, tl);
+#endif
         continue;
       }
       const int64_t d = 3 * (int64_t)c.Kmin;
@@ -1151,16 +1182,25 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   const bool rec_q = rec && rec->q_chain, rec_p = rec && rec->p_chain;
   double phase[7] = {0, 0, 0, 0, 0, 0, 0};
   auto clk = std::chrono::steady_clock::now();
+  int64_t l_now = 0;
   auto lap = [&](int i) {
     const auto t = std::chrono::steady_clock::now();
-    phase[i] += std::chrono::duration<double>(t - clk).count();
+    const double dt = std::chrono::duration<double>(t - clk).count();
+    phase[i] += dt;
     clk = t;
+#ifdef RHMC_RJ_TIMING
+    if (dt > 1e-3)
+      std::fprintf(stderr, "rj slow phase %d: %.3f ms (l %lld)\n", i, dt * 1e3, (long long)l_now);
+#else
+    (void)l_now;
+#endif
   };
   std::vector<int64_t> order, order0, jump, live, scored, acc_rows;
 #ifdef RHMC_RJ_TIMING
   const auto t_loop0 = std::chrono::steady_clock::now();
 #endif
   for (int64_t l = 0; l < rows_n; ++l) {
+    l_now = l;
     if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
     if (cfg->n_beta > 0) R.P.beta = cfg->schedule_beta[std::min<int64_t>(l, cfg->n_beta - 1)];
     const Metric M = R.metric();
@@ -1232,15 +1272,14 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     int32_t kj = 1;
     for (int64_t c : jump) kj = std::max(kj, Kc[c]);
     const int64_t dj = std::min<int64_t>(W, 3 * (int64_t)kj + 3);
-    double* Jq = w->J;              // [nj][dj] q rows, then [nj][dj] p rows
-    double* Jp = w->J + nj * dj;
+    double* Jq = w->Jh_d;           // [nj][dj] q rows, then [nj][dj] p rows (host, mapped)
+    double* Jp = w->Jh_d + nj * dj;
     int64_t* jd = D.idx_d(kIdxJump);
     if (nj > 0) {
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
       if (int rc = rhmc_rows_copy_device(ctx, w->P, W, jd, Jp, dj, nullptr, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "gather");
-      RJ_HIP(hipMemcpyAsync(w->Jh, Jq, (size_t)(2 * nj * dj) * 8, hipMemcpyDeviceToHost, s0));
     }
     RJ_TRY(D.wait(0));
     lap(2);
@@ -1268,16 +1307,43 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       if (!R.ch[c].dead) live.push_back(c);
     for (int64_t c : live) Kc[c] = R.ch[c].K;
     lap(3);
+#ifdef RHMC_RJ_TIMING
+    const auto tq0 = std::chrono::steady_clock::now();
+#endif
     if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
-      RJ_HIP(hipMemcpyAsync(Jq, w->Jh, (size_t)(2 * nj * dj) * 8, hipMemcpyHostToDevice, s0));
+#ifdef RHMC_RJ_TIMING
+      const auto tr1 = std::chrono::steady_clock::now();
+#endif
       if (int rc = rhmc_rows_copy_device(ctx, Jq, dj, nullptr, w->Q, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
       if (int rc = rhmc_rows_copy_device(ctx, Jp, dj, nullptr, w->P, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
+#ifdef RHMC_RJ_TIMING
+      const auto tr2 = std::chrono::steady_clock::now();
+#endif
       RJ_TRY(D.upload_K());
+#ifdef RHMC_RJ_TIMING
+      const auto tr3 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
+      if (ms(tq0, tr3) > 0.2)
+        std::fprintf(stderr, "rj slow rows back: - %.3f (%lld B) scatter %.3f upload_K %.3f ms\n",
+                     ms(tq0, tr1), (long long)(2 * nj * dj * 8), ms(tr1, tr2), ms(tr2, tr3));
+#endif
     }
+#ifdef RHMC_RJ_TIMING
+    const auto tq1 = std::chrono::steady_clock::now();
+#endif
     // 5. the trajectory after the jump
     RJ_TRY(D.trajectories(&R.P, live, cfg->n_steps, kIdxSteps2));
+#ifdef RHMC_RJ_TIMING
+    {
+      const auto tq2 = std::chrono::steady_clock::now();
+      auto ms = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
+      if (ms(tq0, tq2) > 0.2)
+        std::fprintf(stderr, "rj slow steps2 queue: rows back %.3f ms, launches %.3f ms (l %lld)\n",
+                     ms(tq0, tq1), ms(tq1, tq2), (long long)l);
+    }
+#endif
     lap(4);
     // 6. V(q') and T(p', H(q')) of every chain that was not a dead end
     scored.clear();

@@ -108,12 +108,15 @@ def test_native_dead_ends_on_the_engine(gpu_lib):
     assert all(np.isfinite(x).all() and 3 <= x.size <= 12 for x in q)
 
 
-def test_native_two_pipes_equal_one(gpu_lib):
-    """n_pipes = 2 (two halves on two host threads, their host and GPU phases
-    overlapping, each half its own engine batches) gives every chain the same
-    moves, star counts and accepts as one pass, and the same states (the
-    engine's results do not depend on the batch; tolerance for the kernels
-    whose last bits follow wave-mates in rare non-finite / far-off cases)."""
+@pytest.mark.parametrize("pipes", [2, 3, 8])
+def test_native_pipes_equal_one(gpu_lib, pipes):
+    """n_pipes = 2, 3 or 8 (that many parts on as many host threads, their
+    host and GPU phases overlapping, each part its own engine batches; 3 splits
+    64 chains unevenly, 8 puts two parts on each of the box's four hardware
+    queues) gives every chain the same moves, star counts and accepts as one
+    pass, and the same states (the engine's results do not depend on the
+    batch; tolerance for the kernels whose last bits follow wave-mates in rare
+    non-finite / far-off cases)."""
     z = load_golden("rj")
     name = "rj_all"
     par = R.params_from_npz(z, name + "/par_")
@@ -128,7 +131,7 @@ def test_native_two_pipes_equal_one(gpu_lib):
               P_move=[0.4, 0.3, 0.3])
     a, b = make(), make()
     qa = a.run_RHMC_rj_batched([m.copy() for m in starts], list(range(64)), n_pipes=1, **kw)
-    qb = b.run_RHMC_rj_batched([m.copy() for m in starts], list(range(64)), n_pipes=2, **kw)
+    qb = b.run_RHMC_rj_batched([m.copy() for m in starts], list(range(64)), n_pipes=pipes, **kw)
     for k in ("move_chain", "N_chain", "A_chain", "flag_chain"):
         np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
     assert_state_close(a.q_chain, b.q_chain, 1e-12, "q_chain")
