@@ -765,8 +765,9 @@ constexpr int kStreamsPerPipe = 2;  // main (in order) + aux (records, packed gr
     if (int rc_ = (expr)) return rc_;       \
   } while (0)
 
-// Index lists of an iteration, one region each (an async copy reads its pinned
-// source when it executes, so no region is rewritten before a sync).
+// Index lists of an iteration, one region each (the launches read them from
+// mapped host memory when they execute, so no region is rewritten before a
+// wait on its readers).
 enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions };
 
 // One pipe's buffers: device rows and pinned staging, grown as needed and kept
@@ -784,43 +785,39 @@ struct Work {
   hipEvent_t ev[4] = {};
 
   int64_t cap_n = 0, cap_W = 0;
-  // device.  Buffers that cross PCIe in the same phase are adjacent, so each
-  // phase moves them in one copy: `up` = [zoff (N int64) | K (N int32, in N
-  // int64 slots) | Z (M doubles)] (the iteration's host draws), `vt` = [V (N)
-  // | T1 (N)] (V(q') and T(p', H(q')) back together); the jumps' q rows and
-  // p rows sit back to back in Jh (pinned, mapped) below.
-  double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *Ps = nullptr, *Z = nullptr;
-  double *pack = nullptr, *T0 = nullptr, *T1 = nullptr, *V = nullptr;
-  int32_t* Kd = nullptr;
-  int64_t *zoffd = nullptr, *idxd = nullptr;
-  void *up_d = nullptr, *vt_d = nullptr;
-  // pinned host, the same layouts
+  // Device rows: Q, P (the trajectories' state), Q0 (each iteration's start),
+  // pack (the fixed-K launches' gathered batches).
+  double *Q = nullptr, *P = nullptr, *Q0 = nullptr, *pack = nullptr;
+  // Everything that crosses PCIe lives in coherent pinned host memory mapped
+  // into the device's address space, and the kernels read or write it there
+  // (their *_d addresses): the iteration's draws `up` = [zoff (N int64) | K
+  // (N int32, in N int64 slots) | Z (M doubles)], the index lists, T0 | V(q),
+  // V(q') | T', the record rows' live columns and the jumping rows.  No copy
+  // engine and no copy call: SDMA copies stalled a pipe 7-8 ms at its first
+  // large copy of a direction (profiles/r06_rj/, RHMC_RJ_TIMING build), and
+  // each one added a queue hand-off to the iteration's critical path.
+  void *up_h = nullptr, *vt_h = nullptr;
   double *Zh = nullptr, *Jh = nullptr, *recq = nullptr, *recp = nullptr;
-  // Jh's device address: the jump rows cross PCIe without the copy engines —
-  // the gather kernel writes them into Jh and the scatter kernel reads them
-  // back from it (coherent pinned memory, mapped into the device's space).
-  // An SDMA H2D copy of those rows stalled the host 7-8 ms at a pipe's first
-  // iterations (profiles/r06_rj/, RHMC_RJ_TIMING build)
-  double* Jh_d = nullptr;
   double *T0h = nullptr, *T1h = nullptr, *Vh = nullptr;
   int32_t* Kh = nullptr;
   int64_t *zoffh = nullptr, *idxh = nullptr;
-  void *up_h = nullptr, *vt_h = nullptr;
+  // their device addresses
+  double *Zd = nullptr, *Jd = nullptr, *recqd = nullptr, *recpd = nullptr;
+  double *T0d = nullptr, *T1d = nullptr, *Vd = nullptr;
+  int32_t* Kd = nullptr;
+  int64_t *zoffd = nullptr, *idxd = nullptr;
 
   void release() {
-    for (double* d : {Q, P, Q0, Ps, pack, T0}) (void)hipFree(d);
-    for (void* d : {up_d, vt_d}) (void)hipFree(d);
-    (void)hipFree(idxd);
+    for (double* d : {Q, P, Q0, pack}) (void)hipFree(d);
     for (double* h : {Jh, recq, recp, T0h}) (void)hipHostFree(h);
     for (void* h : {up_h, vt_h}) (void)hipHostFree(h);
     (void)hipHostFree(idxh);
-    Q = P = Q0 = Ps = Z = pack = T0 = T1 = V = nullptr;
-    Kd = nullptr;
-    zoffd = idxd = nullptr;
-    up_d = vt_d = up_h = vt_h = nullptr;
-    Zh = Jh = recq = recp = T0h = T1h = Vh = Jh_d = nullptr;
-    Kh = nullptr;
-    zoffh = idxh = nullptr;
+    Q = P = Q0 = pack = nullptr;
+    up_h = vt_h = nullptr;
+    Zh = Jh = recq = recp = T0h = T1h = Vh = nullptr;
+    Zd = Jd = recqd = recpd = T0d = T1d = Vd = nullptr;
+    Kh = Kd = nullptr;
+    zoffh = idxh = zoffd = idxd = nullptr;
     cap_n = cap_W = 0;
   }
 
@@ -858,36 +855,31 @@ struct Work {
     auto dmal = [](auto** p, size_t count) {
       return hipMalloc((void**)p, count * sizeof(**p)) == hipSuccess;
     };
-    auto hmal = [](auto** p, size_t count) {
-      return hipHostMalloc((void**)p, count * sizeof(**p), hipHostMallocDefault) == hipSuccess;
-    };
-    auto hmap = [](auto** p, size_t count) {  // coherent, mapped: kernels read / write it
+    // coherent, mapped: the kernels read / write it at its device address
+    auto hmap = [](auto** p, auto** d, size_t count) {
       return hipHostMalloc((void**)p, count * sizeof(**p),
-                           hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess;
+                           hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess &&
+             hipHostGetDevicePointer((void**)d, *p, 0) == hipSuccess;
     };
-    double *upd = nullptr, *uph = nullptr, *vtd = nullptr, *vth = nullptr;
-    const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&Ps, M) &&
-                    dmal(&upd, 2 * N + M) && dmal(&pack, 4 * M) &&
-                    dmal(&T0, N) && dmal(&vtd, 2 * N) && dmal(&idxd, kIdxRegions * N) &&
-                    hmal(&uph, 2 * N + M) && hmap(&Jh, 2 * M) &&
-                    hipHostGetDevicePointer((void**)&Jh_d, Jh, 0) == hipSuccess && hmal(&recq, M) &&
-                    hmal(&recp, M) && hmal(&T0h, 2 * N) && hmal(&vth, 2 * N) &&
-                    hmal(&idxh, kIdxRegions * N);
-    up_d = upd;
+    double *uph = nullptr, *upd = nullptr, *vth = nullptr, *vtd = nullptr;
+    const bool ok = dmal(&Q, M) && dmal(&P, M) && dmal(&Q0, M) && dmal(&pack, 4 * M) &&
+                    hmap(&uph, &upd, 2 * N + M) && hmap(&Jh, &Jd, 2 * M) &&
+                    hmap(&recq, &recqd, M) && hmap(&recp, &recpd, M) &&
+                    hmap(&T0h, &T0d, 2 * N) && hmap(&vth, &vtd, 2 * N) &&
+                    hmap(&idxh, &idxd, kIdxRegions * N);
     up_h = uph;
-    vt_d = vtd;
     vt_h = vth;
     if (ok) {
-      zoffd = (int64_t*)upd;
-      Kd = (int32_t*)(upd + N);
-      Z = upd + 2 * N;
       zoffh = (int64_t*)uph;
       Kh = (int32_t*)(uph + N);
       Zh = uph + 2 * N;
-      V = vtd;
-      T1 = vtd + N;
+      zoffd = (int64_t*)upd;
+      Kd = (int32_t*)(upd + N);
+      Zd = upd + 2 * N;
       Vh = vth;
       T1h = vth + N;
+      Vd = vtd;
+      T1d = vtd + N;
     }
     if (!ok) {
       release();
@@ -978,31 +970,23 @@ struct DevRun {
   rhmc_ctx* ctx;
   Work* w;
   int64_t n, W;
-  std::vector<int32_t>& K;  // host star counts (mirrored to w->Kd by upload_K)
+  std::vector<int32_t>& K;  // host star counts (what the kernels read: set_K)
   const std::vector<char>& ragged_ok;
 
   int engine_fail(int rc, const char* what) {
     const char* m = rhmc_last_error();
     return fail(rc, std::string("engine ") + what + " failed: " + (m ? m : ""));
   }
-  int upload_K() {
-    std::copy(K.begin(), K.end(), w->Kh);
-    RJ_HIP(hipMemcpyAsync(w->Kd, w->Kh, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice,
-                          w->s[0]));
-    return 0;
-  }
+  // the star counts as the kernels read them (mapped host memory; no kernel
+  // reading them is in flight when the host rewrites them)
+  void set_K() { std::copy(K.begin(), K.end(), w->Kh); }
   int64_t* idx_h(int region) { return w->idxh + region * w->cap_n; }
   int64_t* idx_d(int region) { return w->idxd + region * w->cap_n; }
-  // the plan's chain order as a device index list (main stream); tail > 0:
-  // the copy also carries the next region's first `tail` entries (staged by
-  // the caller), one H2D instead of two
-  int upload_order(const Plan& pl, int region, int64_t tail = 0) {
+  // the plan's chain order as the launches' index list.  Each region is
+  // rewritten only after a wait on the launches that read it (or, for the
+  // commit list, behind them in stream order)
+  void set_order(const Plan& pl, int region) {
     std::copy(pl.order.begin(), pl.order.end(), idx_h(region));
-    const int64_t cnt = tail > 0 ? w->cap_n + tail : (int64_t)pl.order.size();
-    if (cnt > 0)
-      RJ_HIP(hipMemcpyAsync(idx_d(region), idx_h(region), (size_t)cnt * sizeof(int64_t),
-                            hipMemcpyHostToDevice, w->s[0]));
-    return 0;
   }
   // the host waits until stream i is done.  (A blocking-sync event instead of
   // the runtime's spinning wait measured 0.87-0.93x at B4: the wake-up latency
@@ -1020,10 +1004,10 @@ struct DevRun {
 
   // n_steps steps on chains idx (rows of Q, P)
   int trajectories(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t n_steps,
-                   int region, int64_t tail = 0) {
+                   int region) {
     if (idx.empty()) return 0;
     const Plan pl = make_plan(idx, K, ragged_ok);
-    RJ_TRY(upload_order(pl, region, tail));
+    set_order(pl, region);
     bool aux_used = false;
     int packed = 0;
     for (const Call& c : pl.calls) {
@@ -1069,15 +1053,15 @@ struct DevRun {
     return 0;
   }
 
-  // V of chains idx (rows of Q) -> V[j] for chain order[j]; with dst_h also
-  // D2H there on main (not synced)
+  // V of chains idx (rows of Q) -> V_out[j] for chain order[j] (a device
+  // address: the mapped host buffer the host reads after a wait)
   int energies(const rhmc_params* P, const std::vector<int64_t>& idx, int32_t f_pos,
-               std::vector<int64_t>& order, int region, double* dst_h = nullptr) {
+               std::vector<int64_t>& order, int region, double* V_out) {
     order.clear();
     if (idx.empty()) return 0;
     const Plan pl = make_plan(idx, K, ragged_ok);
     order = pl.order;
-    RJ_TRY(upload_order(pl, region));
+    set_order(pl, region);
     for (const Call& c : pl.calls) {
       const int64_t* rows = idx_d(region) + c.off;
       if (c.ragged) {
@@ -1085,7 +1069,7 @@ struct DevRun {
         const auto tl0 = std::chrono::steady_clock::now();
 #endif
         if (int rc = rhmc_energy_ragged_device(ctx, P, w->Q, W, rows, w->Kd, c.n, c.Kmin, c.Kmax,
-                                               f_pos, w->V + c.off, w->s[0]))
+                                               f_pos, V_out + c.off, w->s[0]))
           return engine_fail(rc, "ragged energy");
 #ifdef RHMC_RJ_TIMING
         const double tl = std::chrono::duration<double>(std::chrono::steady_clock::now() - tl0)
@@ -1100,13 +1084,10 @@ struct DevRun {
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, rows, w->pack, d, nullptr, c.n, (int32_t)d,
                                          w->s[0]))
         return engine_fail(rc, "gather");
-      if (int rc = rhmc_energy_device(ctx, P, w->pack, nullptr, w->V + c.off, nullptr, c.n, c.Kmin,
+      if (int rc = rhmc_energy_device(ctx, P, w->pack, nullptr, V_out + c.off, nullptr, c.n, c.Kmin,
                                       f_pos, w->s[0]))
         return engine_fail(rc, "energy");
     }
-    if (dst_h)
-      RJ_HIP(hipMemcpyAsync(dst_h, w->V, pl.order.size() * sizeof(double),
-                            hipMemcpyDeviceToHost, w->s[0]));
     return 0;
   }
 };
@@ -1122,7 +1103,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
 #endif
   const int64_t W = 3 * (int64_t)cfg->N_max;
   RJ_TRY(w->ensure(dev, n, W));
-  hipStream_t s0 = w->s[0], s1 = w->s[1];
+  hipStream_t s0 = w->s[0];
   Run R;
   R.phys = nullptr;
   R.P = *P0;
@@ -1163,8 +1144,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     std::fill(row + 3 * (int64_t)K[c], row + w0, 0.);
   });
   RJ_HIP(hipMemsetAsync(w->Q0, 0, (size_t)(n * W) * 8, s0));
-  RJ_HIP(hipMemcpy2DAsync(w->Q0, (size_t)W * 8, w->Zh, (size_t)w0 * 8, (size_t)w0 * 8,
-                          (size_t)n, hipMemcpyHostToDevice, s0));
+  if (int rc = rhmc_rows_copy_device(ctx, w->Zd, w0, nullptr, w->Q0, W, nullptr, n, (int32_t)w0, s0))
+    return fail(rc, std::string("engine start rows failed: ") +
+                        (rhmc_last_error() ? rhmc_last_error() : ""));
   RJ_HIP(hipStreamSynchronize(s0));  // Zh is the draws' staging next
   std::vector<char> ragged_ok((size_t)cfg->N_max + 1, 0);
   {
@@ -1231,40 +1213,33 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     const int32_t kmax = *std::max_element(Kc.begin(), Kc.end());
     const int64_t wq = std::min<int64_t>(W, 3 * (int64_t)kmax + 3);
     const int64_t wr = 3 * (int64_t)kmax;  // the record rows' live columns
-    std::copy(Kc.begin(), Kc.end(), w->Kh);  // [zoff | K | Z] in one H2D
-    RJ_HIP(hipMemcpyAsync(w->up_d, w->up_h, (size_t)(2 * w->cap_n + zt) * 8,
-                          hipMemcpyHostToDevice, s0));
+    D.set_K();  // [zoff | K | Z] are read by the kernels where the host wrote them
     RJ_HIP(hipMemcpy2DAsync(w->Q, (size_t)W * 8, w->Q0, (size_t)W * 8, (size_t)wq * 8, (size_t)n,
                             hipMemcpyDeviceToDevice, s0));
-    if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, w->Z, w->zoffd, n,
-                                          w->T0, s0))
+    if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, w->Zd, w->zoffd, n,
+                                          w->T0d, s0))
       return D.engine_fail(rc, "momentum");
-    RJ_HIP(hipMemcpyAsync(w->T0h, w->T0, (size_t)n * 8, hipMemcpyDeviceToHost, s0));
+    // the record rows' live columns, before the trajectory moves P
+    if (rec_q)
+      if (int rc = rhmc_rows_copy_device(ctx, w->Q0, W, nullptr, w->recqd, W, nullptr, n,
+                                         (int32_t)wr, s0))
+        return D.engine_fail(rc, "record rows");
     if (rec_p)
-      RJ_HIP(hipMemcpy2DAsync(w->Ps, (size_t)W * 8, w->P, (size_t)W * 8, (size_t)wr * 8,
-                              (size_t)n, hipMemcpyDeviceToDevice, s0));
-    if (rec_q || rec_p) {  // the record rows' live columns leave on the aux stream
-      RJ_TRY(D.join(0, 1, 2));
-      if (rec_q)
-        RJ_HIP(hipMemcpy2DAsync(w->recq, (size_t)W * 8, w->Q0, (size_t)W * 8, (size_t)wr * 8,
-                                (size_t)n, hipMemcpyDeviceToHost, s1));
-      if (rec_p)
-        RJ_HIP(hipMemcpy2DAsync(w->recp, (size_t)W * 8, w->Ps, (size_t)W * 8, (size_t)wr * 8,
-                                (size_t)n, hipMemcpyDeviceToHost, s1));
-    }
+      if (int rc = rhmc_rows_copy_device(ctx, w->P, W, nullptr, w->recpd, W, nullptr, n,
+                                         (int32_t)wr, s0))
+        return D.engine_fail(rc, "record rows");
     const bool reuse = V_end_ok && R.P.g_ff2 == V_end_g_ff2 && R.P.beta == V_end_beta;
-    double* V0h = w->T0h + w->cap_n;  // V(q) when not reused, read at the accept step
-    if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order0, kIdxV0, V0h));
-    // the jumping chains (their rows go to the host after the trajectory):
-    // their index list rides on the trajectory's order upload
-    static_assert(kIdxJump == kIdxSteps1 + 1, "adjacent index regions");
+    // V(q) when not reused, [T0 | V(q)] read at the accept step
+    double* V0h = w->T0h + w->cap_n;
+    if (!reuse) RJ_TRY(D.energies(&R.P, all, cfg->f_pos, order0, kIdxV0, w->T0d + w->cap_n));
+    // the jumping chains (their rows go to the host after the trajectory)
     jump.clear();
     for (int64_t c = 0; c < n; ++c)
       if (R.ch[c].move != 0) jump.push_back(c);
     std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
     // 3. the trajectory of every chain (queued behind the above).  The host
     // needs T0, V(q) and the record rows only at the accept step: no wait here
-    RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1, (int64_t)jump.size()));
+    RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1));
     lap(1);
     // 4. the jumping chains' rows to the host, their proposals on (q, -p), back
     const int64_t nj = (int64_t)jump.size();
@@ -1272,8 +1247,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     int32_t kj = 1;
     for (int64_t c : jump) kj = std::max(kj, Kc[c]);
     const int64_t dj = std::min<int64_t>(W, 3 * (int64_t)kj + 3);
-    double* Jq = w->Jh_d;           // [nj][dj] q rows, then [nj][dj] p rows (host, mapped)
-    double* Jp = w->Jh_d + nj * dj;
+    double* Jq = w->Jd;             // [nj][dj] q rows, then [nj][dj] p rows (host, mapped)
+    double* Jp = w->Jd + nj * dj;
     int64_t* jd = D.idx_d(kIdxJump);
     if (nj > 0) {
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, jd, Jq, dj, nullptr, nj, (int32_t)dj, s0))
@@ -1311,24 +1286,11 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     const auto tq0 = std::chrono::steady_clock::now();
 #endif
     if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
-#ifdef RHMC_RJ_TIMING
-      const auto tr1 = std::chrono::steady_clock::now();
-#endif
       if (int rc = rhmc_rows_copy_device(ctx, Jq, dj, nullptr, w->Q, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
       if (int rc = rhmc_rows_copy_device(ctx, Jp, dj, nullptr, w->P, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
-#ifdef RHMC_RJ_TIMING
-      const auto tr2 = std::chrono::steady_clock::now();
-#endif
-      RJ_TRY(D.upload_K());
-#ifdef RHMC_RJ_TIMING
-      const auto tr3 = std::chrono::steady_clock::now();
-      auto ms = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
-      if (ms(tq0, tr3) > 0.2)
-        std::fprintf(stderr, "rj slow rows back: - %.3f (%lld B) scatter %.3f upload_K %.3f ms\n",
-                     ms(tq0, tr1), (long long)(2 * nj * dj * 8), ms(tr1, tr2), ms(tr2, tr3));
-#endif
+      D.set_K();
     }
 #ifdef RHMC_RJ_TIMING
     const auto tq1 = std::chrono::steady_clock::now();
@@ -1349,15 +1311,11 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     scored.clear();
     for (int64_t c = 0; c < n; ++c)
       if (!R.ch[c].dead) scored.push_back(c);
-    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1));
+    RJ_TRY(D.energies(&R.P, scored, cfg->f_pos, order, kIdxV1, w->Vd));
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, nullptr, nullptr, n,
-                                          w->T1, s0))
+                                          w->T1d, s0))
       return D.engine_fail(rc, "kinetic");
-    // V(q') (order.size() values) and T1 (n) back in one copy: [V | T1]
-    RJ_HIP(hipMemcpyAsync(w->vt_h, w->vt_d, (size_t)(w->cap_n + n) * 8, hipMemcpyDeviceToHost,
-                          s0));
-    RJ_TRY(D.wait(0));
-    RJ_TRY(D.wait(1));  // the record rows of the iteration's start
+    RJ_TRY(D.wait(0));  // V(q'), T', and the iteration's T0, V(q) and record rows
     for (size_t j = 0; j < order.size(); ++j) V1[order[j]] = w->Vh[j];
     if (reuse) {
       V0 = V_end;
@@ -1419,8 +1377,6 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       const int64_t dc = std::min<int64_t>(W, 3 * (int64_t)kacc);
       int64_t* cd = D.idx_d(kIdxCommit);
       std::copy(acc_rows.begin(), acc_rows.end(), D.idx_h(kIdxCommit));
-      RJ_HIP(hipMemcpyAsync(cd, D.idx_h(kIdxCommit), acc_rows.size() * 8, hipMemcpyHostToDevice,
-                            s0));
       if (int rc = rhmc_rows_copy_device(ctx, w->Q, W, cd, w->Q0, W, cd,
                                          (int64_t)acc_rows.size(), (int32_t)dc, s0))
         return D.engine_fail(rc, "commit");
@@ -1437,8 +1393,9 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   int32_t kout = 1;
   for (int64_t c = 0; c < n; ++c) kout = std::max(kout, R.ch[c].K);
   const int64_t w1 = 3 * (int64_t)kout;
-  RJ_HIP(hipMemcpy2DAsync(w->Zh, (size_t)w1 * 8, w->Q0, (size_t)W * 8, (size_t)w1 * 8,
-                          (size_t)n, hipMemcpyDeviceToHost, s0));
+  if (int rc = rhmc_rows_copy_device(ctx, w->Q0, W, nullptr, w->Zd, w1, nullptr, n, (int32_t)w1,
+                                     s0))
+    return D.engine_fail(rc, "final rows");
   RJ_HIP(hipStreamSynchronize(s0));
   R.parallel(all, [&](int64_t c) {
     put_row(q + c * W, w->Zh + c * w1, 3 * (int64_t)R.ch[c].K, W, W);
