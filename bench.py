@@ -361,7 +361,7 @@ def bench_rj(args, wl, gpu, world, rank):
     # every chain starts with K0 stars: one [n, K0, 3] array (run_RHMC_rj_batched
     # packs it in one native pass)
     starts = np.stack(starts)
-    seeds = [1000 * rank + c for c in range(n_chains)]
+    seeds = 1000 * rank + np.arange(n_chains, dtype=np.int64)
     # successive runs write their q_chain / p_chain records into the previous
     # run's arrays (opt-in: no page faults on fresh memory inside the timing)
     kw["reuse_records"] = True
@@ -372,7 +372,7 @@ def bench_rj(args, wl, gpu, world, rank):
     steps = 0
     t0 = time.perf_counter()
     for i in range(args.steps):
-        g.run_RHMC_rj_batched(starts, [s + 7 * (i + 1) for s in seeds],      # (starts unchanged)
+        g.run_RHMC_rj_batched(starts, seeds + 7 * (i + 1),                   # (starts unchanged)
                               n_pipes=args.rj_pipes, **kw)
         # move 0: one trajectory; a jump: two, unless its proposal was a dead end
         steps += int(np.sum(np.where((g.move_chain == 0) | (g.flag_chain != 0), 1, 2))) * leap

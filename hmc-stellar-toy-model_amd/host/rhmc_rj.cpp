@@ -94,7 +94,7 @@ void put_row(double* dst, const double* src, int64_t d, int64_t zero_to, int64_t
 // at the larger of that and the new width d; else the whole row
 int64_t zero_end(const rhmc_rj_config* cfg, const rhmc_rj_record* rec, int64_t r, int64_t d,
                  int64_t W) {
-  if (!cfg->records_zero_padded) return W;
+  if (!(cfg->records_zero_padded & RHMC_RJ_ZP_RECORDS)) return W;
   const int32_t old = rec->n_stars[r];
   if (old < 1 || old > cfg->N_max) return W;
   return std::max(d, 3 * (int64_t)old);
@@ -499,8 +499,8 @@ struct Run {
 int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, const int32_t* K,
           const uint32_t* seeds, int64_t n) {
   if (!P || !cfg) return fail(RHMC_ERR_ARG, "params or config is NULL");
-  if (cfg->records_zero_padded != 0 && cfg->records_zero_padded != 1)
-    return fail(RHMC_ERR_ARG, "records_zero_padded must be 0 or 1");
+  if (cfg->records_zero_padded < 0 || cfg->records_zero_padded > 3)
+    return fail(RHMC_ERR_ARG, "records_zero_padded must be in [0, 3]");
   if (cfg->n_pipes < 0 || cfg->n_pipes > kMaxPipes)
     return fail(RHMC_ERR_ARG, "n_pipes must be in [0, 8]");
   if (n < 0) return fail(RHMC_ERR_ARG, "n < 0");
@@ -536,7 +536,7 @@ int check(const rhmc_params* P, const rhmc_rj_config* cfg, const double* q, cons
 }
 
 int check_records(const rhmc_rj_config* cfg, const rhmc_rj_record* rec) {
-  if (cfg->records_zero_padded && !(rec && rec->n_stars))
+  if ((cfg->records_zero_padded & RHMC_RJ_ZP_RECORDS) && !(rec && rec->n_stars))
     return fail(RHMC_ERR_ARG, "records_zero_padded needs the n_stars record");
   return 0;
 }
@@ -1119,6 +1119,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.pool = w->pool.get();
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
+  const std::vector<int32_t> K_in(K, K + n);  // the rows' widths on entry (ZP_STARTS)
   std::vector<int64_t> all((size_t)n);
   int32_t kin = 1;
   for (int64_t c = 0; c < n; ++c) {
@@ -1398,7 +1399,11 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     return D.engine_fail(rc, "final rows");
   RJ_HIP(hipStreamSynchronize(s0));
   R.parallel(all, [&](int64_t c) {
-    put_row(q + c * W, w->Zh + c * w1, 3 * (int64_t)R.ch[c].K, W, W);
+    // ZP_STARTS: the caller's row is zero past 3 K_in, so the zeros stop there
+    const int64_t d = 3 * (int64_t)R.ch[c].K;
+    put_row(q + c * W, w->Zh + c * w1, d,
+            (cfg->records_zero_padded & RHMC_RJ_ZP_STARTS) ? std::max(d, 3 * (int64_t)K_in[c]) : W,
+            W);
     _mm_sfence();
     const Chain& h = R.ch[c];
     K[c] = h.K;
@@ -1602,6 +1607,11 @@ int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, do
 
 int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
                         double flux_to_count, double* q) {
+  return rhmc_rj_pack_starts_padded(rows, K, n, N_max, flux_to_count, q, nullptr);
+}
+
+int rhmc_rj_pack_starts_padded(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
+                               double flux_to_count, double* q, const int32_t* K_prev) {
   if (n < 0 || N_max < 1) return fail(RHMC_ERR_ARG, "bad n or N_max");
   if (n > 0 && (!rows || !K || !q)) return fail(RHMC_ERR_ARG, "rows, K or q is NULL");
   const int64_t W = 3 * (int64_t)N_max;
@@ -1617,22 +1627,45 @@ int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t
     at[c + 1] = at[c] + 3 * (int64_t)K[c];
   }
   auto pack = [&](int64_t c0, int64_t c1) {
+    std::vector<double> tmp((size_t)W);
+    // pow is a pure function: a small direct-mapped memo of magnitudes (the
+    // flagship starts every chain from the same model stars)
+    uint64_t memo_key[64];
+    double memo_val[64];
+    bool memo_ok[64] = {};
     for (int64_t c = c0; c < c1; ++c) {
-      double* row = q + c * W;
       const double* src = rows + at[c];
       for (int32_t k = 0; k < K[c]; ++k) {
         const double v = src[3 * k];
         // mag2flux_converter (sampler_RHMC.py:147-152, utils.py:24-25): libm pow,
         // the function NumPy's and Python's float power call
-        row[3 * k] = flux_to_count > 0 ? std::pow(10.0, 0.4 * (22.5 - v)) * flux_to_count : v;
-        row[3 * k + 1] = src[3 * k + 1];
-        row[3 * k + 2] = src[3 * k + 2];
+        double f = v;
+        if (flux_to_count > 0) {
+          uint64_t bits;
+          std::memcpy(&bits, &v, 8);
+          const int slot = (int)((bits * 0x9E3779B97F4A7C15ull) >> 58);
+          if (!memo_ok[slot] || memo_key[slot] != bits) {
+            memo_key[slot] = bits;
+            memo_val[slot] = std::pow(10.0, 0.4 * (22.5 - v));
+            memo_ok[slot] = true;
+          }
+          f = memo_val[slot] * flux_to_count;
+        }
+        tmp[3 * k] = f;
+        tmp[3 * k + 1] = src[3 * k + 1];
+        tmp[3 * k + 2] = src[3 * k + 2];
       }
-      std::fill(row + 3 * (int64_t)K[c], row + W, 0.);
+      // zero-padded (streamed), or only up to the row's old width
+      const int64_t d = 3 * (int64_t)K[c];
+      const int32_t kp = K_prev ? K_prev[c] : 0;
+      put_row(q + c * W, tmp.data(), d, kp >= 1 && kp <= N_max ? std::max(d, 3 * (int64_t)kp) : W,
+              W);
     }
+    _mm_sfence();
   };
-  // a few host threads for large batches (one pow per star); chains split in
-  // contiguous ranges, so the result does not depend on the thread count
+  // a few host threads for large batches (one pow per distinct magnitude, a
+  // 3 N_max row of stores per chain); chains split in contiguous ranges, so
+  // the result does not depend on the thread count
   const int64_t work = at[n];
   const int nt = (int)std::min<int64_t>(8, std::max<int64_t>(1, work / 60000));
   std::vector<std::thread> th;

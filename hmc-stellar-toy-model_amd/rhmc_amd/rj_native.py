@@ -20,7 +20,8 @@ LIB_PATH = os.environ.get("RHMC_RJ_LIB",
 DEAD_END = 1                 # RHMC_RJ_DEAD_END
 
 EXPORTS = ("rhmc_rj_run", "rhmc_rj_run_physics", "rhmc_np_draws", "rhmc_rj_beta_eval",
-           "rhmc_rj_pack_starts", "rhmc_rj_release", "rhmc_rj_last_error")
+           "rhmc_rj_pack_starts", "rhmc_rj_pack_starts_padded", "rhmc_rj_release",
+           "rhmc_rj_last_error")
 
 ENERGY_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.POINTER(capi.RhmcParams),
                              ctypes.POINTER(ctypes.c_double), ctypes.c_int64, ctypes.c_int32,
@@ -95,6 +96,8 @@ def _load():
                           ctypes.c_int64, vp],
         "rhmc_rj_beta_eval": [ctypes.c_double, ctypes.c_double, vp, ctypes.c_int64, vp, vp],
         "rhmc_rj_pack_starts": [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, vp],
+        "rhmc_rj_pack_starts_padded": [vp, vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_double, vp,
+                                       vp],
         "rhmc_rj_release": [ctypes.c_int32],
     }
     for name, args in sig.items():
@@ -171,13 +174,16 @@ def _q_buf(out, n, N_max):
     return np.empty(shape)
 
 
-def pack_starts(q_models, N_max, flux_to_count=0., out=None):
+def pack_starts(q_models, N_max, flux_to_count=0., out=None, K_prev=None):
     """Chain starts -> (q [n][3 N_max] zero-padded, K [n]) in one native pass.
     q_models: [K_c, 3] arrays, or one [n, K, 3] array when every chain has K
     stars — (mag, x, y) rows converted by format_q's mag2flux
     (sampler_RHMC.py:209-217, bit-identical) when flux_to_count > 0 — or flat
     flux-count vectors with flux_to_count = 0.  out: an optional float64
-    [n][3 N_max] buffer that takes q (every row written in full)."""
+    [n][3 N_max] buffer that takes q (every row written in full), or with
+    K_prev (int32 [n]: out's rows are zero past 3 K_prev[c] — the previous
+    run's final q and K) each row's zeros only up to its old width.  The
+    rows come back zero past 3 K[c] (rhmc_rj_config ZP_STARTS)."""
     n = len(q_models)
     if n == 0:
         return np.zeros((0, 3 * int(N_max))), np.zeros(0, np.int32)
@@ -189,8 +195,7 @@ def pack_starts(q_models, N_max, flux_to_count=0., out=None):
             raise ValueError("every start needs 1 .. N_max stars")
         rows = np.ascontiguousarray(q_models, dtype=np.float64).reshape(-1)
         q = _q_buf(out, n, N_max)
-        _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
-                                        float(flux_to_count), q.ctypes.data))
+        _pack(rows, K, n, N_max, flux_to_count, q, out, K_prev)
         return q, K
     flat = [np.asarray(m, dtype=np.float64) for m in q_models]
     if all(m.ndim == 2 and m.shape[1] == 3 for m in flat):      # [K, 3] rows
@@ -206,14 +211,23 @@ def pack_starts(q_models, N_max, flux_to_count=0., out=None):
         raise ValueError("every start needs 1 .. N_max stars")
     rows = np.ascontiguousarray(rows, dtype=np.float64)
     q = _q_buf(out, n, N_max)
-    _check(_lib.rhmc_rj_pack_starts(rows.ctypes.data, K.ctypes.data, n, int(N_max),
-                                    float(flux_to_count), q.ctypes.data))
+    _pack(rows, K, n, N_max, flux_to_count, q, out, K_prev)
     return q, K
+
+
+def _pack(rows, K, n, N_max, flux_to_count, q, out, K_prev):
+    kp = None
+    if (q is out and isinstance(K_prev, np.ndarray) and K_prev.dtype == np.int32
+            and K_prev.shape == (n,) and K_prev.flags.c_contiguous):
+        kp = K_prev.ctypes.data
+    _check(_lib.rhmc_rj_pack_starts_padded(rows.ctypes.data, K.ctypes.data, n, int(N_max),
+                                           float(flux_to_count), q.ctypes.data, kp))
 
 
 def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, cols, fmin, fmax,
         K_split, beta_a, beta_b, schedule_g_ff2=None, schedule_beta=None, ctx=None, physics=None,
-        n_threads=0, n_pipes=0, states=None, packed=None, out=None, zero_padded=False):
+        n_threads=0, n_pipes=0, states=None, packed=None, out=None, zero_padded=False,
+        starts_zero_padded=False):
     """Run the native RJ sampler.  q_models: list of [3 K_c] flux-count q
     vectors, or None with packed = (q [n][3 N_max], K [n]) from pack_starts.  Either ctx (a capi.Context: the engine) or physics (a pair of
     Python callables energy(q[n,3K], f_pos) -> V[n] and steps(q, p, n_steps)
@@ -224,7 +238,9 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     allocated; "n_stars" [n_iter+1][n] int32 likewise).  zero_padded: the
     out q_chain / p_chain rows are zero past 3 out["n_stars"][row] (the
     previous run's records: rhmc_rj_config::records_zero_padded), so only
-    the columns a row can have used are rewritten.  Returns (q list, record dict); record["states"] holds every chain's stream
+    the columns a row can have used are rewritten.  starts_zero_padded:
+    packed's q rows are zero past 3 K[c] (pack_starts leaves them so), so the
+    final rows' zeros are written only up to the starting width.  Returns (q list, record dict); record["states"] holds every chain's stream
     at the end (pass it back as `states` to resume)."""
     W = 3 * int(N_max)
     if packed is not None:
@@ -235,6 +251,7 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
             raise ValueError("packed q must be [n][3 N_max]")
     else:
         q, K = pack_starts(q_models, N_max)
+        starts_zero_padded = True
     n = K.size
     if states is None and (seeds is None or len(seeds) != n):
         raise ValueError("one seed per chain")
@@ -267,7 +284,7 @@ def run(params, q_models, seeds, n_iter, n_steps, N_max, P_move, f_pos, rows, co
     pm = (ctypes.c_double * 3)(*[float(v) for v in P_move])
     cfg = RjConfig(int(n_iter), int(n_steps), int(N_max), int(f_pos), int(rows), int(cols),
                    int(n_threads), ng, nb, int(n_pipes), int(states is not None),
-                   int(bool(zero_padded)), pm,
+                   (1 if zero_padded else 0) | (2 if starts_zero_padded else 0), pm,
                    float(fmin), float(fmax), float(K_split), float(beta_a), float(beta_b), sg,
                    sb, st.ctypes.data if n else None)
     rows_n = int(n_iter) + 1

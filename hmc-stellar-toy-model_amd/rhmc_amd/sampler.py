@@ -868,24 +868,27 @@ class multi_gym(base_class):
         # With reuse_records the previous run's packed [n][3 N_max] array takes
         # them when nothing else holds it (the returned q views keep it alive)
         qbuf = self.__dict__.get("_rj_qbuf") if reuse_records else None
+        kbuf = self.__dict__.get("_rj_kbuf") if reuse_records else None
         if not (isinstance(qbuf, np.ndarray) and sys.getrefcount(qbuf) <= 3):
-            qbuf = None
-        self._rj_qbuf = None
+            qbuf = kbuf = None
+        self._rj_qbuf = self._rj_kbuf = None
         if isinstance(q_models_0, np.ndarray) and q_models_0.ndim == 3:
-            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf)
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf,
+                                           K_prev=kbuf)
             dims = None
         else:
             dims = {np.ndim(m) for m in q_models_0}
         if dims is None:
             pass
         elif dims <= {2}:
-            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf)
+            packed = rj_native.pack_starts(q_models_0, N_max, self.flux_to_count, out=qbuf,
+                                           K_prev=kbuf)
         elif dims <= {1}:
-            packed = rj_native.pack_starts(q_models_0, N_max, out=qbuf)
+            packed = rj_native.pack_starts(q_models_0, N_max, out=qbuf, K_prev=kbuf)
         else:
             packed = rj_native.pack_starts([self._start_q(m) for m in q_models_0], N_max,
-                                           out=qbuf)
-        qbuf = None
+                                           out=qbuf, K_prev=kbuf)
+        qbuf = kbuf = None
         P = self._params(delta, counter_max, for_energy=True)
         # reuse_records (opt-in): the previous run's q_chain / p_chain memory
         # takes this run's records when nothing but this sampler holds it (no
@@ -923,7 +926,7 @@ class multi_gym(base_class):
             n_pipes=n_pipes, states=(None if rng_states is None else
                                      rng_states if isinstance(rng_states, np.ndarray)
                                      else rj_native.states_from(rng_states)), packed=packed,
-            out=out, zero_padded=padded and "n_stars" in out)
+            out=out, zero_padded=padded and "n_stars" in out, starts_zero_padded=True)
         out = None
         self.rj_native_s = time.perf_counter() - t0     # the library call (records included)
         n_it = Niter + 1
@@ -938,7 +941,7 @@ class multi_gym(base_class):
         self.flag_chain = rec["flags"]
         self.rj_rng_states = rec["states"]     # every chain's stream at the end (resume)
         if reuse_records:
-            self._rj_qbuf = packed[0]
+            self._rj_qbuf, self._rj_kbuf = packed   # final q rows, zero past 3 K
             self._rj_nstars = rec["n_stars"]
             self.q_chain.flags.writeable = False
             self.p_chain.flags.writeable = False

@@ -111,12 +111,16 @@ typedef struct rhmc_rj_config {
   int32_t use_states;    /* 1: the chains' streams start from states[c] instead of
                             seeds[c] (a checkpoint of an earlier run, or any
                             RandomState's get_state(): continue its stream)        */
-  int32_t records_zero_padded; /* 0, or 1: the caller's q_chain / p_chain rows are
-                            zero past 3 n_stars[r] on entry, n_stars holding the
-                            counts of the rows they hold (a previous run's records
-                            of this shape, or zeros: any width is zero-padded past
-                            3); the driver then writes a row's zeros only up to its
-                            old width.  Needs rec->n_stars.  Was `reserved` (0)  */
+  int32_t records_zero_padded; /* bits (0: none; was `reserved`), claims about the
+                            caller's buffers that let the driver write a row's
+                            zeros only up to its old width.  RHMC_RJ_ZP_RECORDS:
+                            the q_chain / p_chain rows are zero past 3 n_stars[r]
+                            on entry, n_stars holding the counts of the rows they
+                            hold (a previous run's records of this shape, or
+                            zeros: then any width is claimed; needs
+                            rec->n_stars).  RHMC_RJ_ZP_STARTS: q's rows are
+                            zero past 3 K[c] on entry (rhmc_rj_pack_starts
+                            leaves them so)                                      */
   double P_move[3];      /* within / birth-death / split-merge probabilities         */
   double fmin, fmax;     /* power-law flux prior range, counts (:1221)               */
   double K_split;        /* split offset scale (:1300)                               */
@@ -155,6 +159,8 @@ typedef struct rhmc_rj_record {
 } rhmc_rj_record;
 
 #define RHMC_RJ_DEAD_END 1u  /* the proposal could not be formed; rejected */
+#define RHMC_RJ_ZP_RECORDS 1  /* rhmc_rj_config::records_zero_padded bits */
+#define RHMC_RJ_ZP_STARTS 2
 
 /*
  * Run n_iter + 1 iterations on n chains.  q: host [n][3 N_max], chain c's
@@ -189,6 +195,13 @@ int rhmc_np_draws(uint32_t seed, int32_t kind, double a, double b, int64_t n, do
  * NumPy scalars use: bit-identical); 0: the rows are already counts. */
 int rhmc_rj_pack_starts(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
                         double flux_to_count, double* q);
+
+/* The same into a q whose rows are zero past 3 K_prev[c] (the previous
+ * run's final rows and counts, e.g.): each row's zeros are written only up to
+ * max(3 K[c], 3 K_prev[c]).  K_prev NULL, or an entry outside [1, N_max]:
+ * whole rows. */
+int rhmc_rj_pack_starts_padded(const double* rows, const int32_t* K, int64_t n, int32_t N_max,
+                               double flux_to_count, double* q, const int32_t* K_prev);
 
 /* The split / merge moves' Beta(beta_a, beta_b) density as the driver
  * evaluates it (scipy.stats.beta.logpdf / pdf at sampler_RHMC.py:1342, :1363,

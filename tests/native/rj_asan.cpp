@@ -248,9 +248,9 @@ int main(int argc, char** argv) {
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "P_move sum");
     c = config(2, 4, 0.5, 0.25, 0.25);
-    c.records_zero_padded = 2;
+    c.records_zero_padded = 4;
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
-          "records_zero_padded 2");
+          "records_zero_padded 4");
     c.records_zero_padded = 1;  // needs the n_stars record
     CHECK(rhmc_rj_run_physics(&phys, &P, &c, q.data(), &K, &s, 1, nullptr) == RHMC_ERR_ARG,
           "records_zero_padded without n_stars");

@@ -327,3 +327,25 @@ def test_integration_stub_matches_the_config_layout(rj):
     assert [f[0] for f in A._fields_] == [f[0] for f in B._fields_]
     assert ctypes.sizeof(A) == ctypes.sizeof(B)
     assert all(getattr(A, f[0]).offset == getattr(B, f[0]).offset for f in B._fields_)
+
+
+def test_pack_starts_padded_equals_full(rj):
+    """rhmc_rj_pack_starts_padded: rows written into a buffer that is zero past
+    3 K_prev[c] (the previous run's final rows) equal a full pack, zeros
+    included, whether a row grew or shrank; without K_prev, a buffer of
+    garbage is overwritten whole."""
+    rs = np.random.RandomState(4)
+    n, N_max = 40, 12
+    old = [rs.rand(k, 3) * 5 + 15 for k in rs.randint(1, N_max + 1, n)]
+    new = [rs.rand(k, 3) * 5 + 15 for k in rs.randint(1, N_max + 1, n)]
+    q_old, K_old = rj.pack_starts(old, N_max, 1.5)
+    fresh, K_new = rj.pack_starts(new, N_max, 1.5)
+    q, K = rj.pack_starts(new, N_max, 1.5, out=q_old, K_prev=K_old)
+    assert q is q_old and np.array_equal(K, K_new)
+    assert np.array_equal(q, fresh)
+    junk = np.full_like(fresh, 9.)
+    q2, _ = rj.pack_starts(new, N_max, 1.5, out=junk)
+    assert np.array_equal(q2, fresh)
+    same = np.repeat(new[0][None], 30, axis=0)      # one model for every chain (the memo)
+    qs, _ = rj.pack_starts(same, N_max, 1.5)
+    assert np.array_equal(qs, np.repeat(fresh[:1], 30, axis=0))
