@@ -175,13 +175,19 @@ struct BetaDist {
 };
 
 // ------------------------------------------------------------- thread pool
-// Fork-join pool that lives for one run: the workers sleep between phases
-// (spawning threads per phase cost ~3 ms per iteration at 16 threads).
+// Fork-join pool shared by every pipe of a run (and kept between runs: spawning
+// threads per phase cost ~3 ms per iteration at 16 threads, per run ~1 ms).
+// Several callers may run jobs at once: a worker takes chunks of whichever job
+// has some left, so while one pipe waits for its GPU phase its share of the
+// host threads works on the other pipes' host phases (round 5's per-pipe
+// pools left them idle), and a pipe thread waiting for its stream takes chunks
+// too (help()).  Each chain's work is its own, so results do not depend on
+// which thread runs it.
 class Pool {
  public:
-  explicit Pool(int n) {
+  explicit Pool(int workers) {
     try {
-      for (int t = 1; t < n; ++t) th_.emplace_back([this] { worker(); });
+      for (int t = 0; t < workers; ++t) th_.emplace_back([this] { worker(); });
     } catch (...) {  // a thread could not start: stop and join the ones that did
       shutdown();
       throw;
@@ -189,31 +195,76 @@ class Pool {
   }
   ~Pool() { shutdown(); }
   int size() const { return (int)th_.size() + 1; }
-  // body(i) for i in [0, n), chunks of 16, the caller works too.  An exception
-  // from body (any thread) is rethrown here once every thread has left it.
+  // body(i) for i in [0, n), in chunks, the caller works too.  An exception
+  // from body (any thread) is rethrown here once no thread is left in it.
   void run(int64_t n, const std::function<void(int64_t)>& body) {
+    Job j;
+    j.body = &body;
+    j.n = n;
     {
       std::lock_guard<std::mutex> l(mu_);
-      body_ = &body;
-      n_ = n;
-      next_.store(0);
-      busy_ = (int)th_.size();
-      exc_ = nullptr;
-      ++gen_;
+      jobs_.push_back(&j);
     }
     cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> l(mu_);
-    done_.wait(l, [this] { return busy_ == 0; });
-    body_ = nullptr;
-    if (exc_) {
-      std::exception_ptr e = exc_;
-      exc_ = nullptr;
-      std::rethrow_exception(e);
+    while (take(j)) {
     }
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &j));
+    }
+    // every chunk is taken; wait for the ones still running elsewhere (no
+    // worker picks the job up once it is off the list)
+    while (j.done.load() != n || j.users.load() != 0) std::this_thread::yield();
+    if (j.exc) std::rethrow_exception(j.exc);
+  }
+  // one chunk of any caller's job, if one is left: false if none
+  bool help() {
+    Job* j = nullptr;
+    {
+      std::lock_guard<std::mutex> l(mu_);
+      j = pick();
+      if (j) j->users.fetch_add(1);
+    }
+    if (!j) return false;
+    const bool did = take(*j);
+    j->users.fetch_sub(1);
+    return did;
   }
 
  private:
+  static constexpr int64_t kChunk = 16;
+  struct Job {
+    const std::function<void(int64_t)>* body = nullptr;
+    int64_t n = 0;
+    std::atomic<int64_t> next{0}, done{0};
+    std::atomic<int> users{0};
+    std::atomic<bool> failed{false};
+    std::mutex emu;
+    std::exception_ptr exc;
+  };
+  Job* pick() {  // mu_ held
+    for (Job* j : jobs_)
+      if (j->next.load() < j->n) return j;
+    return nullptr;
+  }
+  // one chunk of j; false when none was left.  After a failure the remaining
+  // chunks are counted without running (the first exception is kept)
+  bool take(Job& j) {
+    const int64_t b = j.next.fetch_add(kChunk);
+    if (b >= j.n) return false;
+    const int64_t e = std::min(j.n, b + kChunk);
+    if (!j.failed.load()) {
+      try {
+        for (int64_t i = b; i < e; ++i) (*j.body)(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> l(j.emu);
+        if (!j.exc) j.exc = std::current_exception();
+        j.failed.store(true);
+      }
+    }
+    j.done.fetch_add(e - b);
+    return true;
+  }
   void shutdown() {
     {
       std::lock_guard<std::mutex> l(mu_);
@@ -223,45 +274,37 @@ class Pool {
     for (auto& t : th_) t.join();
     th_.clear();
   }
-  void work() {
-    try {
-      for (;;) {
-        const int64_t b = next_.fetch_add(16);
-        if (b >= n_) return;
-        const int64_t e = std::min(n_, b + 16);
-        for (int64_t i = b; i < e; ++i) (*body_)(i);
-      }
-    } catch (...) {  // keep the first; the other chunks still drain
-      std::lock_guard<std::mutex> l(mu_);
-      if (!exc_) exc_ = std::current_exception();
-      next_.store(n_);
-    }
-  }
   void worker() {
-    uint64_t seen = 0;
     for (;;) {
+      Job* j = nullptr;
       {
         std::unique_lock<std::mutex> l(mu_);
-        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(l, [&] { return stop_ || (j = pick()) != nullptr; });
         if (stop_) return;
-        seen = gen_;
+        j->users.fetch_add(1);
       }
-      work();
-      std::lock_guard<std::mutex> l(mu_);
-      if (--busy_ == 0) done_.notify_one();
+      while (take(*j)) {
+      }
+      j->users.fetch_sub(1);
     }
   }
   std::vector<std::thread> th_;
   std::mutex mu_;
-  std::condition_variable cv_, done_;
-  const std::function<void(int64_t)>* body_ = nullptr;
-  int64_t n_ = 0;
-  std::atomic<int64_t> next_{0};
-  int busy_ = 0;
-  uint64_t gen_ = 0;
+  std::condition_variable cv_;
+  std::vector<Job*> jobs_;
   bool stop_ = false;
-  std::exception_ptr exc_;
 };
+
+// The process's pools by worker count, kept for its lifetime (a run takes the
+// one of its size; runs on other threads may share it)
+std::shared_ptr<Pool> shared_pool(int workers) {
+  static std::mutex mu;
+  static std::map<int, std::shared_ptr<Pool>> pools;
+  std::lock_guard<std::mutex> l(mu);
+  auto& p = pools[workers];
+  if (!p) p = std::make_shared<Pool>(workers);
+  return p;
+}
 
 // ------------------------------------------------------------------- chains
 struct Chain {
@@ -548,11 +591,11 @@ int host_threads(const rhmc_rj_config* cfg) {
 }
 
 // n chains (a contiguous slice of the caller's: q, K, seeds point at its
-// first chain); record row l of chain c is l * rec_stride + rec_off + c; nt
-// host threads; the phase times are added to phase_out[7].
+// first chain); record row l of chain c is l * rec_stride + rec_off + c; the
+// host work on `pool`; the phase times are added to phase_out[7].
 int run(const rhmc_rj_physics* phys, const rhmc_params* P0,
         const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
-        const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
+        const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, Pool* pool,
         double* phase_out) {
   if (!phys || !phys->energy || !phys->steps) return fail(RHMC_ERR_ARG, "physics is NULL");
   Run R;
@@ -561,9 +604,8 @@ int run(const rhmc_rj_physics* phys, const rhmc_params* P0,
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
   R.beta.set(cfg->beta_a, cfg->beta_b);
-  R.nt = nt;
-  Pool pool(nt);
-  R.pool = &pool;
+  R.nt = pool->size();
+  R.pool = pool;
   R.ch.resize((size_t)n);
   const int64_t W = 3 * (int64_t)cfg->N_max;
   std::vector<int64_t> all((size_t)n);
@@ -777,10 +819,6 @@ enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions
 struct Work {
   std::mutex mu;
   int dev = -1;
-  // the pipe's host worker threads, kept between runs like the buffers
-  // (starting 16 threads per run cost ~1 ms); rebuilt when the count changes
-  std::unique_ptr<Pool> pool;
-  int pool_n = 0;
   hipStream_t s[kStreamsPerPipe] = {};
   hipEvent_t ev[4] = {};
 
@@ -823,8 +861,6 @@ struct Work {
 
   // everything, streams and events included (rhmc_rj_release; `mu` held)
   void destroy() {
-    pool.reset();
-    pool_n = 0;
     if (dev < 0) return;
     (void)hipSetDevice(dev);
     for (auto& st : s)
@@ -991,9 +1027,17 @@ struct DevRun {
   // the host waits until stream i is done.  (A blocking-sync event instead of
   // the runtime's spinning wait measured 0.87-0.93x at B4: the wake-up latency
   // costs more than the CPU the spin takes from the pool threads.)
+  // While the stream runs, the waiting pipe thread takes host chunks of the
+  // other pipes' phases.
+  Pool* pool;
   int wait(int i) {
-    RJ_HIP(hipStreamSynchronize(w->s[i]));
-    return 0;
+    for (;;) {
+      const hipError_t e = hipStreamQuery(w->s[i]);
+      if (e == hipSuccess) return 0;
+      if (e != hipErrorNotReady)
+        return fail(RHMC_ERR_HIP, std::string("reversible-jump stream: ") + hipGetErrorString(e));
+      if (!pool->help()) std::this_thread::yield();
+    }
   }
   // aux waits for main, or main for aux
   int join(int from, int to, int e) {
@@ -1096,7 +1140,7 @@ struct DevRun {
 // its first chain; record row l of chain c is l * rec_stride + rec_off + c).
 int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
                const rhmc_rj_config* cfg, double* q, int32_t* K, const uint32_t* seeds, int64_t n,
-               const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, int nt,
+               const rhmc_rj_record* rec, int64_t rec_stride, int64_t rec_off, Pool* pool,
                double* phase_out) {
 #ifdef RHMC_RJ_TIMING
   const auto t_setup0 = std::chrono::steady_clock::now();
@@ -1110,13 +1154,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.cfg = cfg;
   R.Kmax = cfg->N_max;
   R.beta.set(cfg->beta_a, cfg->beta_b);
-  R.nt = nt;
-  if (!w->pool || w->pool_n != nt) {
-    w->pool.reset();
-    w->pool.reset(new Pool(nt));
-    w->pool_n = nt;
-  }
-  R.pool = w->pool.get();
+  R.nt = pool->size();
+  R.pool = pool;
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
   const std::vector<int32_t> K_in(K, K + n);  // the rows' widths on entry (ZP_STARTS)
@@ -1157,7 +1196,7 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       ragged_ok[k] = (char)ok;
     }
   }
-  DevRun D{ctx, w, n, W, Kc, ragged_ok};
+  DevRun D{ctx, w, n, W, Kc, ragged_ok, pool};
   const int64_t rows_n = (int64_t)cfg->n_iter + 1;
   std::vector<double> V0((size_t)n), V1((size_t)n), V_end((size_t)n);
   double V_end_g_ff2 = 0., V_end_beta = 0.;
@@ -1424,16 +1463,17 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
 }
 
 // Split n chains into `pipes` contiguous parts run concurrently, part i on
-// its own host thread (part 0 on the caller's) with its share of the nt pool
-// threads: body(i, first chain, count, threads, phase[7]) -> rc.  The first
-// failing part's error is the one reported.
+// its own host thread (part 0 on the caller's), all on one shared pool of
+// nt - pipes workers: body(i, first chain, count, pool, phase[7]) -> rc.  The
+// first failing part's error is the one reported.
 template <class Body>
 int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
+  const std::shared_ptr<Pool> pool = shared_pool(std::max(0, nt - std::max(1, pipes)));
   // one part's body on this thread; an exception becomes an error code (no
   // C++ exception may cross the ABI, and none may leave a std::thread)
-  auto guarded = [&](int i, int64_t f, int64_t m, int t, double* ph, std::string& err) {
+  auto guarded = [&](int i, int64_t f, int64_t m, double* ph, std::string& err) {
     try {
-      const int rc = body(i, f, m, t, ph);
+      const int rc = body(i, f, m, pool.get(), ph);
       if (rc) err = g_err;
       return rc;
     } catch (const std::exception& e) {
@@ -1445,14 +1485,12 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
   };
   if (pipes <= 1) {
     std::string err;
-    const int rc = guarded(0, 0, n, nt, phase, err);
+    const int rc = guarded(0, 0, n, phase, err);
     if (rc) g_err = err;
     return rc;
   }
   std::vector<int64_t> first((size_t)pipes + 1);
   for (int i = 0; i <= pipes; ++i) first[i] = n * i / pipes;
-  std::vector<int> threads((size_t)pipes);
-  for (int i = 0; i < pipes; ++i) threads[i] = std::max(1, nt * (i + 1) / pipes - nt * i / pipes);
   std::vector<std::array<double, 7>> ph((size_t)pipes);
   std::vector<int> rcs((size_t)pipes, 0);
   std::vector<std::string> errs((size_t)pipes);
@@ -1462,7 +1500,7 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
     ph[i].fill(0.);
     try {
       ts.emplace_back([&, i] {
-        rcs[i] = guarded(i, first[i], first[i + 1] - first[i], threads[i], ph[i].data(), errs[i]);
+        rcs[i] = guarded(i, first[i], first[i + 1] - first[i], ph[i].data(), errs[i]);
       });
     } catch (const std::exception& e) {  // this part does not run: report it
       rcs[i] = RHMC_ERR_NOMEM;
@@ -1470,7 +1508,7 @@ int run_pipes(int pipes, int64_t n, int nt, double* phase, Body body) {
     }
   }
   ph[0].fill(0.);
-  rcs[0] = guarded(0, first[0], first[1] - first[0], threads[0], ph[0].data(), errs[0]);
+  rcs[0] = guarded(0, first[0], first[1] - first[0], ph[0].data(), errs[0]);
   for (auto& t : ts) t.join();
   for (int i = 0; i < pipes; ++i)
     for (int k = 0; k < 7; ++k) phase[k] += ph[i][k];
@@ -1513,9 +1551,9 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
     // with pipes > 1 the callbacks are called from that many threads at once
     const int64_t W = 3 * (int64_t)cfg->N_max;
     int rc = run_pipes(cfg->n_pipes > 1 ? pipes_for(cfg, n) : 1, n, nt, phase,
-                       [&](int, int64_t f, int64_t m, int t, double* ph) {
+                       [&](int, int64_t f, int64_t m, Pool* pool, double* ph) {
                          return run(phys, P, cfg, q + f * W, K + f,
-                                    seeds ? seeds + f : nullptr, m, rec, n, f, t, ph);
+                                    seeds ? seeds + f : nullptr, m, rec, n, f, pool, ph);
                        });
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
@@ -1527,6 +1565,12 @@ int rhmc_rj_run_physics(const rhmc_rj_physics* phys, const rhmc_params* P,
 int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, double* q,
                 int32_t* K, const uint32_t* seeds, int64_t n, const rhmc_rj_record* rec) {
   if (!ctx) return fail(RHMC_ERR_ARG, "ctx is NULL");
+#ifdef RHMC_RJ_TIMING
+  const auto t_entry = std::chrono::steady_clock::now();
+  auto ms_since = [&] {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t_entry).count() * 1e3;
+  };
+#endif
   try {
     if (int rc = check(P, cfg, q, K, seeds, n)) return rc;
     if (int rc = check_records(cfg, rec)) return rc;
@@ -1549,12 +1593,21 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
     }
     const int64_t W = 3 * (int64_t)cfg->N_max;
     double phase[7] = {0, 0, 0, 0, 0, 0, 0};
-    const int rc = run_pipes(pipes, n, nt, phase, [&](int i, int64_t f, int64_t m, int t,
+#ifdef RHMC_RJ_TIMING
+    std::fprintf(stderr, "rj run: pipes start at %.3f ms\n", ms_since());
+#endif
+    const int rc = run_pipes(pipes, n, nt, phase, [&](int i, int64_t f, int64_t m, Pool* pool,
                                                       double* ph) {
+#ifdef RHMC_RJ_TIMING
+      std::fprintf(stderr, "rj run: pipe %d starts at %.3f ms\n", i, ms_since());
+#endif
       if (hipSetDevice(dev) != hipSuccess) return fail(RHMC_ERR_HIP, "hipSetDevice failed");
       return run_device(ctx, dev, works[i], P, cfg, q + f * W, K + f, seeds ? seeds + f : nullptr,
-                        m, rec, n, f, t, ph);
+                        m, rec, n, f, pool, ph);
     });
+#ifdef RHMC_RJ_TIMING
+    std::fprintf(stderr, "rj run: pipes joined at %.3f ms\n", ms_since());
+#endif
     if (rc == 0 && rec && rec->phase_s) std::copy(phase, phase + 7, rec->phase_s);
     return rc;
   } catch (const std::exception& e) {
