@@ -819,6 +819,9 @@ enum { kIdxV0, kIdxSteps1, kIdxJump, kIdxSteps2, kIdxV1, kIdxCommit, kIdxRegions
 struct Work {
   std::mutex mu;
   int dev = -1;
+  // the pipe's per-chain host state, kept between runs with its vectors'
+  // capacity (freeing and reallocating it per run cost ~2 ms at 1,024 chains)
+  std::vector<Chain> chains;
   hipStream_t s[kStreamsPerPipe] = {};
   hipEvent_t ev[4] = {};
 
@@ -861,6 +864,7 @@ struct Work {
 
   // everything, streams and events included (rhmc_rj_release; `mu` held)
   void destroy() {
+    std::vector<Chain>().swap(chains);
     if (dev < 0) return;
     (void)hipSetDevice(dev);
     for (auto& st : s)
@@ -1156,6 +1160,12 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
   R.beta.set(cfg->beta_a, cfg->beta_b);
   R.nt = pool->size();
   R.pool = pool;
+  struct GiveBack {  // the chains' storage returns to the pipe on every exit
+    std::vector<Chain>& from;
+    std::vector<Chain>& to;
+    ~GiveBack() { from.swap(to); }
+  } give_back{R.ch, w->chains};
+  R.ch.swap(w->chains);
   R.ch.resize((size_t)n);
   std::vector<int32_t> Kc((size_t)n);
   const std::vector<int32_t> K_in(K, K + n);  // the rows' widths on entry (ZP_STARTS)
@@ -1602,8 +1612,12 @@ int rhmc_rj_run(rhmc_ctx* ctx, const rhmc_params* P, const rhmc_rj_config* cfg, 
       std::fprintf(stderr, "rj run: pipe %d starts at %.3f ms\n", i, ms_since());
 #endif
       if (hipSetDevice(dev) != hipSuccess) return fail(RHMC_ERR_HIP, "hipSetDevice failed");
-      return run_device(ctx, dev, works[i], P, cfg, q + f * W, K + f, seeds ? seeds + f : nullptr,
-                        m, rec, n, f, pool, ph);
+      const int rc_i = run_device(ctx, dev, works[i], P, cfg, q + f * W, K + f,
+                                  seeds ? seeds + f : nullptr, m, rec, n, f, pool, ph);
+#ifdef RHMC_RJ_TIMING
+      std::fprintf(stderr, "rj run: pipe %d returns at %.3f ms\n", i, ms_since());
+#endif
+      return rc_i;
     });
 #ifdef RHMC_RJ_TIMING
     std::fprintf(stderr, "rj run: pipes joined at %.3f ms\n", ms_since());
