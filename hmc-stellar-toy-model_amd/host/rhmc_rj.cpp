@@ -315,6 +315,14 @@ struct Chain {
   bool grow = false, dead = false;
   double E0 = 0., factor = 0.;
   std::vector<double> H, tmp, cdf;
+  // the device driver's draws made ahead, while the GPU runs: the accept
+  // uniform, and the next iteration's normals / move / grow of a chain whose
+  // star count cannot change (move 0 or a dead end) — the stream's order is
+  // unchanged, only the time of the draws moves
+  double u = 0.;
+  bool pre = false, grow_next = false;
+  int move_next = 0;
+  std::vector<double> znext;
 };
 
 struct Run {
@@ -1043,6 +1051,16 @@ struct DevRun {
       if (!pool->help()) std::this_thread::yield();
     }
   }
+  // the host waits for event e (recorded on a stream), taking pool chunks
+  int wait_event(int e) {
+    for (;;) {
+      const hipError_t r = hipEventQuery(w->ev[e]);
+      if (r == hipSuccess) return 0;
+      if (r != hipErrorNotReady)
+        return fail(RHMC_ERR_HIP, std::string("reversible-jump event: ") + hipGetErrorString(r));
+      if (!pool->help()) std::this_thread::yield();
+    }
+  }
   // aux waits for main, or main for aux
   int join(int from, int to, int e) {
     RJ_HIP(hipEventRecord(w->ev[e], w->s[from]));
@@ -1231,6 +1249,18 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
 #ifdef RHMC_RJ_TIMING
   const auto t_loop0 = std::chrono::steady_clock::now();
 #endif
+  // an iteration's first draws (:1021-1022, :1031-1033): z = randn(3K), the
+  // move type, grow / shrink
+  auto draw_start = [&](Chain& h, double* z) {
+    for (int64_t i = 0; i < 3 * (int64_t)h.K; ++i) z[i] = h.rng.gauss();
+    h.move = (int)choice(h.rng, cfg->P_move, 3, h.cdf);
+    h.grow = false;
+    if (h.move != 0) {
+      const double half[2] = {0.5, 0.5};
+      h.grow = choice(h.rng, half, 2, h.cdf) == 0;  // [True, False]
+    }
+  };
+  for (auto& h : R.ch) h.pre = false;
   for (int64_t l = 0; l < rows_n; ++l) {
     l_now = l;
     if (cfg->n_g_ff2 > 0) R.P.g_ff2 = cfg->schedule_g_ff2[std::min<int64_t>(l, cfg->n_g_ff2 - 1)];
@@ -1245,12 +1275,13 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
       double* z = w->Zh + w->zoffh[c];
-      for (int64_t i = 0; i < 3 * (int64_t)h.K; ++i) z[i] = h.rng.gauss();
-      h.move = (int)choice(h.rng, cfg->P_move, 3, h.cdf);
-      h.grow = false;
-      if (h.move != 0) {
-        const double half[2] = {0.5, 0.5};
-        h.grow = choice(h.rng, half, 2, h.cdf) == 0;  // [True, False]
+      if (h.pre) {  // drawn during the previous iteration's V(q') wait
+        std::copy(h.znext.begin(), h.znext.end(), z);
+        h.move = h.move_next;
+        h.grow = h.grow_next;
+        h.pre = false;
+      } else {
+        draw_start(h, z);
       }
       h.K0 = h.K;
       h.dead = false;
@@ -1289,8 +1320,35 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
     // 3. the trajectory of every chain (queued behind the above).  The host
     // needs T0, V(q) and the record rows only at the accept step: no wait here
+    RJ_HIP(hipEventRecord(w->ev[0], s0));  // T0, V(q) and the record rows are in
     RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1));
     lap(1);
+    // while the trajectories run: the iteration's record rows (row l: its
+    // starting state; none of it depends on the accept step)
+    RJ_TRY(D.wait_event(0));
+    if (!reuse)
+      for (size_t j = 0; j < order0.size(); ++j) V0[order0[j]] = V0h[j];
+    else
+      V0 = V_end;
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      const int64_t r = l * rec_stride + rec_off + c;
+      h.E0 = V0[c] + w->T0h[c];
+      if (!rec) return;
+      // the rows are zero past 3 K0 on the device: copy the 3 K0, write the
+      // zeros (read n_stars[r] before it is rewritten)
+      const int64_t d = 3 * (int64_t)h.K0, zt = zero_end(cfg, rec, r, d, W);
+      if (rec_q) put_row(rec->q_chain + r * W, w->recq + c * W, d, zt, W);
+      if (rec_p) put_row(rec->p_chain + r * W, w->recp + c * W, d, zt, W);
+      _mm_sfence();
+      if (rec->V_chain) rec->V_chain[r] = V0[c];
+      if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
+      if (rec->E_chain) rec->E_chain[r] = h.E0;
+      if (rec->n_stars) rec->n_stars[r] = h.K0;
+      if (rec->move)
+        rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
+    });
+    lap(6);
     // 4. the jumping chains' rows to the host, their proposals on (q, -p), back
     const int64_t nj = (int64_t)jump.size();
     // a jumping row's columns: its 3 K stars and the one a birth / split adds
@@ -1365,39 +1423,42 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     if (int rc = rhmc_kinetic_rows_device(ctx, &R.P, w->Q, w->P, W, w->Kd, nullptr, nullptr, n,
                                           w->T1d, s0))
       return D.engine_fail(rc, "kinetic");
-    RJ_TRY(D.wait(0));  // V(q'), T', and the iteration's T0, V(q) and record rows
+    lap(4);
+    // while they run: each scored chain's accept uniform (:1072, :1120), and
+    // for a chain whose star count cannot change the next iteration's draws
+    const bool next = l + 1 < rows_n;
+    R.parallel(all, [&](int64_t c) {
+      Chain& h = R.ch[c];
+      if (h.dead) {
+        h.K = h.K0;
+      } else {
+        h.u = std::log(h.rng.random_sample());
+        if (h.move != 0) return;
+      }
+      if (!next) return;
+      const int mv = h.move;  // this iteration's, for its accept step
+      const bool gr = h.grow;
+      h.znext.resize(3 * (size_t)h.K);
+      draw_start(h, h.znext.data());
+      h.move_next = h.move;
+      h.grow_next = h.grow;
+      h.move = mv;
+      h.grow = gr;
+      h.pre = true;
+    });
+    lap(0);
+    RJ_TRY(D.wait(0));  // V(q') and T'
     for (size_t j = 0; j < order.size(); ++j) V1[order[j]] = w->Vh[j];
-    if (reuse) {
-      V0 = V_end;
-    } else {
-      for (size_t j = 0; j < order0.size(); ++j) V0[order0[j]] = V0h[j];
-    }
     lap(5);
-    // 7. the iteration's records (row l: its starting state), accept / reject
-    // (:1072-1083, :1120-1131); accepted rows become Q0
+    // 7. accept / reject (:1072-1083, :1120-1131); accepted rows become Q0
     std::vector<char> acc((size_t)n, 0);
     R.parallel(all, [&](int64_t c) {
       Chain& h = R.ch[c];
       const int64_t r = l * rec_stride + rec_off + c;
-      h.E0 = V0[c] + w->T0h[c];
-      if (rec) {
-        // the rows are zero past 3 K0 on the device: copy the 3 K0, write the
-        // zeros (read n_stars[r] before it is rewritten)
-        const int64_t d = 3 * (int64_t)h.K0, zt = zero_end(cfg, rec, r, d, W);
-        if (rec_q) put_row(rec->q_chain + r * W, w->recq + c * W, d, zt, W);
-        if (rec_p) put_row(rec->p_chain + r * W, w->recp + c * W, d, zt, W);
-        _mm_sfence();
-        if (rec->V_chain) rec->V_chain[r] = V0[c];
-        if (rec->T_chain) rec->T_chain[r] = w->T0h[c];
-        if (rec->E_chain) rec->E_chain[r] = h.E0;
-        if (rec->n_stars) rec->n_stars[r] = h.K0;
-        if (rec->move)
-          rec->move[r] = h.move == 0 ? 0 : h.move == 1 ? (h.grow ? 1 : 2) : (h.grow ? 3 : 4);
-      }
       bool a = false;
       if (!h.dead) {
         const double E1 = V1[c] + w->T1h[c];
-        const double u = std::log(h.rng.random_sample());
+        const double u = h.u;
         if (h.move == 0) {
           const double dE = E1 - h.E0;
           a = (dE < 0) || (u < -dE);
