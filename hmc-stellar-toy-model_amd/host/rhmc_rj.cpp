@@ -1335,12 +1335,13 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
     std::copy(jump.begin(), jump.end(), D.idx_h(kIdxJump));
     // 3. the trajectory of every chain (queued behind the above).  The host
     // needs T0, V(q) and the record rows only at the accept step: no wait here
-    RJ_HIP(hipEventRecord(w->ev[0], s0));  // T0, V(q) and the record rows are in
+    RJ_HIP(hipEventRecord(w->ev[2], s0));  // T0, V(q) and the record rows are in
+                                           // (events 0 and 1: join())
     RJ_TRY(D.trajectories(&R.P, all, cfg->n_steps, kIdxSteps1));
     lap(1);
     // while the trajectories run: the iteration's record rows (row l: its
     // starting state; none of it depends on the accept step)
-    RJ_TRY(D.wait_event(0));
+    RJ_TRY(D.wait_event(2));
     if (!reuse)
       for (size_t j = 0; j < order0.size(); ++j) V0[order0[j]] = V0h[j];
     else
