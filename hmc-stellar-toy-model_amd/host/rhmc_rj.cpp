@@ -1406,9 +1406,6 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
       if (!R.ch[c].dead) live.push_back(c);
     for (int64_t c : live) Kc[c] = R.ch[c].K;
     lap(3);
-#ifdef RHMC_RJ_TIMING
-    const auto tq0 = std::chrono::steady_clock::now();
-#endif
     if (nj > 0) {  // every jumping row back (a dead end's rows are restored later)
       if (int rc = rhmc_rows_copy_device(ctx, Jq, dj, nullptr, w->Q, W, jd, nj, (int32_t)dj, s0))
         return D.engine_fail(rc, "scatter");
@@ -1416,20 +1413,8 @@ int run_device(rhmc_ctx* ctx, int dev, Work* w, const rhmc_params* P0,
         return D.engine_fail(rc, "scatter");
       D.set_K();
     }
-#ifdef RHMC_RJ_TIMING
-    const auto tq1 = std::chrono::steady_clock::now();
-#endif
     // 5. the trajectory after the jump
     RJ_TRY(D.trajectories(&R.P, live, cfg->n_steps, kIdxSteps2));
-#ifdef RHMC_RJ_TIMING
-    {
-      const auto tq2 = std::chrono::steady_clock::now();
-      auto ms = [](auto a, auto b) { return std::chrono::duration<double>(b - a).count() * 1e3; };
-      if (ms(tq0, tq2) > 0.2)
-        std::fprintf(stderr, "rj slow steps2 queue: rows back %.3f ms, launches %.3f ms (l %lld)\n",
-                     ms(tq0, tq1), ms(tq1, tq2), (long long)l);
-    }
-#endif
     lap(4);
     // 6. V(q') and T(p', H(q')) of every chain that was not a dead end
     scored.clear();
