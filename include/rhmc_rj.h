@@ -33,12 +33,18 @@
  * Concurrency: each pipe of a run uses device buffers and two HIP streams of
  * its own, held (a mutex) for the whole run, so concurrent rhmc_rj_run calls
  * on one device serialise pipe by pipe; the caller's current device is
- * restored on return.
+ * restored on return.  The pipes' host work runs on one process-wide thread
+ * pool per size (n_threads - pipes workers, kept for the process's lifetime,
+ * shared by concurrent runs); the pipe threads take its chunks while their
+ * streams run.  Host <-> device data moves through coherent pinned host
+ * memory mapped into the device (the engine's kernels read and write it at
+ * its device address): no copy-engine transfers.
  *
- * Retention: those buffers (per device and pipe index, grown to the largest
- * run so far: ~90 MB of HBM and ~60 MB of pinned host memory per pipe at
- * 4,096 chains and N_max 120, 8 pipes from 16,384 chains) stay allocated
- * after a run, so the next run starts without allocating;
+ * Retention: those buffers and the chains' host state (per device and pipe
+ * index, grown to the largest run so far: ~90 MB of HBM and ~60 MB of pinned
+ * host memory per pipe at 4,096 chains and N_max 120, 8 pipes from 16,384
+ * chains) stay allocated after a run, so the next run starts without
+ * allocating;
  * rhmc_rj_release(device) frees them (device < 0: every device), waiting for
  * a run that holds one.
  *
@@ -100,7 +106,8 @@ typedef struct rhmc_rj_config {
   int32_t N_max;         /* record width 3 N_max; star counts stay in [1, N_max]     */
   int32_t f_pos;         /* V's f_pos bits (RHMC_V_FLUX_WALL = run_RHMC f_pos=True)  */
   int32_t rows, cols;    /* num_rows / num_cols (birth positions, :1219-1220)       */
-  int32_t n_threads;     /* host worker threads; <= 0: min(hardware threads, 16)    */
+  int32_t n_threads;     /* host threads, the pipe threads included; <= 0:
+                            min(hardware threads, 16)                             */
   int32_t n_g_ff2;       /* schedule_g_ff2 length (0: none)                          */
   int32_t n_beta;        /* schedule_beta length (0: none)                           */
   int32_t n_pipes;       /* 1: one pass over all chains per phase; 2..8: the chains in
