@@ -31,18 +31,24 @@
 #include <vector>
 
 #include "rhmc.h"
+#ifndef RHMC_KERNELS_ONLY  // (their non-template kernels belong to this unit only)
 #include "rhmc_datagen.hpp"
 #include "rhmc_mh.hpp"
+#endif
 #include "rhmc_tiledl.hpp"
 #include "rhmc_tiledr.hpp"
 #include "rhmc_tiledrk.hpp"
+#ifndef RHMC_KERNELS_ONLY
 #include "rhmc_mhk1.hpp"
 #include "rhmc_mhpk.hpp"
+#endif
 #include "rhmc_pixk.hpp"
 #include "rhmc_wave.hpp"
 #include "rhmc_windowed.hpp"
 #include "rhmc_dense.hpp"
+#ifndef RHMC_KERNELS_ONLY
 #include "rhmc_rows.hpp"
+#endif
 
 namespace rhmc {
 
@@ -1004,8 +1010,17 @@ __global__ void __launch_bounds__(256) energy_win_kernel(EnergyArgs a) {
   if (lane == 0) a.V[chain] = v;
 }
 
+#ifndef RHMC_KERNELS_ONLY
+// The dense kernel's one-slot leapfrog (K <= 64 on 32/48-px images: B4, the
+// reference's big-sim4 run) is compiled in rhmc_dense_ilp.hip with the max-ILP
+// scheduler; this translation unit only launches it.
+extern template __global__ void leapfrog_win_kernel<DenseG<32>, 1>(LeapArgs);
+extern template __global__ void leapfrog_win_kernel<DenseG<48>, 1>(LeapArgs);
+#endif
+
 }  // namespace rhmc
 
+#ifndef RHMC_KERNELS_ONLY
 // ============================================================================
 // Host side: C-ABI
 // ============================================================================
@@ -3181,3 +3196,4 @@ int rhmc_debug_table_seen(uint64_t* out9) {
 }
 #endif
 }  // extern "C"
+#endif  // RHMC_KERNELS_ONLY

@@ -18,20 +18,31 @@ def _disassemble(tmp_path):
     tools = [os.path.join(LLVM, t) for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump")]
     if not all(os.path.exists(t) for t in tools) or not os.path.exists(so):
         pytest.skip("ROCm llvm tools or librhmc.so not available")
-    fat, co = str(tmp_path / "fat.bin"), str(tmp_path / "k.co")
+    fat = str(tmp_path / "fat.bin")
     subprocess.run([tools[0], "--dump-section=.hip_fatbin=" + fat, so], check=True)
-    subprocess.run([tools[1], "--unbundle", "--type=o", "--input=" + fat,
-                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
-    out = subprocess.run([tools[2], "-d", "--mcpu=gfx950", co], check=True,
-                         capture_output=True, text=True).stdout
-    funcs, cur = {}, None
-    for line in out.splitlines():
-        m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
-        if m:
-            cur = m.group(1)
-            funcs[cur] = []
-        elif cur:
-            funcs[cur].append(line)
+    # one offload bundle per translation unit (csrc/rhmc_kernels.hip and
+    # csrc/rhmc_dense_ilp.hip), concatenated by the linker
+    data = open(fat, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    starts = [m.start() for m in re.finditer(re.escape(magic), data)]
+    assert starts, "no offload bundle in .hip_fatbin"
+    funcs = {}
+    for i, st in enumerate(starts):
+        part, co = str(tmp_path / ("b%d.bin" % i)), str(tmp_path / ("k%d.co" % i))
+        open(part, "wb").write(data[st:starts[i + 1] if i + 1 < len(starts) else len(data)])
+        subprocess.run([tools[1], "--unbundle", "--type=o", "--input=" + part,
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
+        out = subprocess.run([tools[2], "-d", "--mcpu=gfx950", co], check=True,
+                             capture_output=True, text=True).stdout
+        cur = None
+        for line in out.splitlines():
+            m = re.match(r"^[0-9a-f]+ <(\S+)>:", line)
+            if m:
+                cur = m.group(1)
+                assert cur not in funcs, "kernel in two code objects: " + cur
+                funcs[cur] = []
+            elif cur:
+                funcs[cur].append(line)
     return funcs
 
 
